@@ -1,0 +1,264 @@
+"""Generate the golden parity fixtures by running the REFERENCE learner (nicholasburden/pymarl) in this container.
+
+    python tests/golden/make_golden.py            # writes tests/golden/*.npz
+
+Not part of the product and never run on the GPU box (it needs /root/reference). It imports the reference's hot
+path from /root/reference/src (those modules import with torch + numpy only), feeds it the seeded
+synthetic replay of pymarl_amd/utils/synthetic.py with numpy-seeded weights loaded via load_state_dict, and records:
+
+* per-step loss and the five learner stats exactly as QLearner.train logs them (q_learner.py:109-116),
+* the sampled episode ids of ReplayBuffer.sample under np.random.seed(2) (episode_buffer.py:291-298),
+* the double-Q greedy actions and their top-2 margins (q_learner.py:71-76),
+* for the small shapes, every intermediate of train() (mac_out ... td), the clipped gradients after step 0,
+  and parameters + RMSprop state after each step,
+* greedy BasicMAC.select_actions(test_mode=True) outputs (basic_controller.py:30-38).
+
+Intermediates are produced by re-running lines 39-97 of q_learner.py on the reference's own MAC / mixer modules
+(same weights, no grad) just before each train() call; that restatement is checked against the loss train()
+itself logs.
+
+Workarounds: default.yaml is missing, so `args` is built explicitly with upstream-PyMARL
+values; `scheme["obs"]["vshape_decoded"]` is required by this fork's BasicMAC._get_input_shape.
+"""
+from __future__ import annotations
+
+import os
+import sys
+from types import SimpleNamespace as SN
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF_SRC = "/root/reference/src"
+sys.path.insert(0, REPO)
+sys.path.insert(0, REF_SRC)
+
+import torch as th  # noqa: E402
+
+from pymarl_amd.utils.synthetic import (agent_param_shapes, init_params, make_replay,  # noqa: E402
+                                        qmix_param_shapes)
+
+from components.episode_buffer import ReplayBuffer  # noqa: E402  (reference)
+from components.transforms import OneHot  # noqa: E402  (reference)
+from controllers.basic_controller import BasicMAC  # noqa: E402  (reference)
+from learners.q_learner import QLearner  # noqa: E402  (reference)
+
+
+class _Console:
+    def info(self, *a, **k):
+        pass
+
+
+class _Logger:
+    def __init__(self):
+        self.console_logger = _Console()
+        self.stats = {}
+
+    def log_stat(self, key, value, t):
+        if isinstance(value, th.Tensor):
+            value = value.item()
+        self.stats.setdefault(key, []).append(float(value))
+
+
+def make_args(n, A, O, S, mixer, H=64, E=32):
+    return SN(n_agents=n, n_actions=A, state_shape=S, obs_shape=O, rnn_hidden_dim=H, mixing_embed_dim=E,
+              mixer=mixer, lr=5e-4, optim_alpha=0.99, optim_eps=1e-5, grad_norm_clip=10.0, gamma=0.99,
+              double_q=True, target_update_interval=200, learner_log_interval=0,
+              obs_last_action=True, obs_agent_id=True, agent="rnn", mac="basic_mac", agent_output_type="q",
+              action_selector="epsilon_greedy", epsilon_start=1.0, epsilon_finish=0.05, epsilon_anneal_time=50000,
+              action_input_representation=None, obs_decoder=None, avail_actions_encoder=None,
+              device="cpu", use_cuda=False)
+
+
+def make_scheme(n, A, O, S):
+    return {
+        "state": {"vshape": S},
+        "obs": {"vshape": O, "group": "agents", "vshape_decoded": O},
+        "actions": {"vshape": (1,), "group": "agents", "dtype": th.long},
+        "avail_actions": {"vshape": (A,), "group": "agents", "dtype": th.int},
+        "reward": {"vshape": (1,)},
+        "terminated": {"vshape": (1,), "dtype": th.uint8},
+    }
+
+
+def build(case):
+    n, A, O, S, T = case["n"], case["A"], case["O"], case["S"], case["T"]
+    args = make_args(n, A, O, S, case["mixer"])
+    scheme = make_scheme(n, A, O, S)
+    groups = {"agents": n}
+    preprocess = {"actions": ("actions_onehot", [OneHot(out_dim=A)])}
+    buf = ReplayBuffer(scheme, groups, case["n_episodes"], T + 1, preprocess=preprocess, device="cpu")
+    data = make_replay(case["n_episodes"], T, n, A, O, S, seed=case["data_seed"], ragged=case["ragged"])
+    for k, v in data.items():
+        buf.data.transition_data[k][:] = th.from_numpy(v)
+    buf.episodes_in_buffer = case["n_episodes"]
+    buf.buffer_index = 0
+
+    mac = BasicMAC(buf.scheme, groups, args)
+    logger = _Logger()
+    learner = QLearner(mac, buf.scheme, logger, args)
+    I = O + A + n
+    w_agent = init_params(agent_param_shapes(I, 64, A), seed=case["weight_seed"])
+    mac.agent.load_state_dict({k: th.from_numpy(v) for k, v in w_agent.items()})
+    learner.target_mac.agent.load_state_dict({k: th.from_numpy(v) for k, v in w_agent.items()})
+    if case["mixer"] == "qmix":
+        w_mix = init_params(qmix_param_shapes(S, n, 32), seed=case["weight_seed"] + 100)
+        learner.mixer.load_state_dict({k: th.from_numpy(v) for k, v in w_mix.items()})
+        learner.target_mixer.load_state_dict({k: th.from_numpy(v) for k, v in w_mix.items()})
+    return args, buf, mac, learner, logger
+
+
+@th.no_grad()
+def intermediates(learner, batch):
+    """q_learner.py:39-97 re-run on the reference's own modules (no grad); returns numpy copies."""
+    args = learner.args
+    rewards = batch["reward"][:, :-1]
+    actions = batch["actions"][:, :-1]
+    terminated = batch["terminated"][:, :-1].float()
+    mask = batch["filled"][:, :-1].float()
+    mask[:, 1:] = mask[:, 1:] * (1 - terminated[:, :-1])
+    avail_actions = batch["avail_actions"]
+    mac_out = []
+    learner.mac.init_hidden(batch.batch_size)
+    for t in range(batch.max_seq_length):
+        mac_out.append(learner.mac.forward(batch, t=t))
+    mac_out = th.stack(mac_out, dim=1)
+    chosen = th.gather(mac_out[:, :-1], dim=3, index=actions).squeeze(3)
+    tmo = []
+    learner.target_mac.init_hidden(batch.batch_size)
+    for t in range(batch.max_seq_length):
+        tmo.append(learner.target_mac.forward(batch, t=t))
+    tmo = th.stack(tmo[1:], dim=1)
+    tmo[avail_actions[:, 1:] == 0] = -9999999
+    mod = mac_out.clone().detach()
+    mod[avail_actions == 0] = -9999999
+    cur_max = mod[:, 1:].max(dim=3, keepdim=True)[1]
+    top2 = th.topk(mod[:, 1:], 2, dim=3)[0]
+    margin = (top2[..., 0] - top2[..., 1])
+    target_max = th.gather(tmo, 3, cur_max).squeeze(3)
+    if learner.mixer is not None:
+        q_tot = learner.mixer(chosen, batch["state"][:, :-1])
+        tq_tot = learner.target_mixer(target_max, batch["state"][:, 1:])
+    else:
+        q_tot, tq_tot = chosen, target_max
+    targets = rewards + args.gamma * (1 - terminated) * tq_tot
+    td = q_tot - targets
+    m = mask.expand_as(td)
+    loss = ((td * m) ** 2).sum() / m.sum()
+    f = lambda x: x.detach().cpu().numpy().copy()  # noqa: E731
+    return dict(mac_out=f(mac_out), target_mac_out=f(tmo), cur_max_actions=f(cur_max.squeeze(3)).astype(np.int64),
+                margin=f(margin), chosen=f(chosen), target_max=f(target_max), q_tot=f(q_tot),
+                target_q_tot=f(tq_tot), targets=f(targets), td=f(td), mask=f(mask), loss=float(loss))
+
+
+def flat_params(learner):
+    ps = [p.detach().cpu().numpy().ravel() for p in learner.params]
+    return np.concatenate(ps).astype(np.float32)
+
+
+def flat_targets(learner):
+    ps = [p.detach().cpu().numpy().ravel() for p in learner.target_mac.agent.parameters()]
+    if learner.mixer is not None:
+        ps += [p.detach().cpu().numpy().ravel() for p in learner.target_mixer.parameters()]
+    return np.concatenate(ps).astype(np.float32)
+
+
+def flat_grads(learner):
+    return np.concatenate([p.grad.detach().cpu().numpy().ravel() for p in learner.params]).astype(np.float32)
+
+
+def flat_sqavg(learner):
+    st = learner.optimiser.state
+    return np.concatenate([st[p]["square_avg"].cpu().numpy().ravel() for p in learner.params]).astype(np.float32)
+
+
+def run_case(name, case):
+    th.set_num_threads(8)
+    args, buf, mac, learner, logger = build(case)
+    np.random.seed(case["sampler_seed"])
+    out = {k: np.array(v) for k, v in case.items() if not isinstance(v, str)}
+    out["mixer"] = np.array(case["mixer"])
+    out["params_init"] = flat_params(learner)
+    ids_all, losses, full = [], [], case["full"]
+    cur_max_steps, margin_steps = [], []
+    per_step = {"params": [], "targets": [], "sqavg": []}
+    episodes = case["episodes"]
+    for k in range(case["steps"]):
+        st = np.random.get_state()
+        batch = buf.sample(case["B"])
+        after = np.random.get_state()
+        np.random.set_state(st)
+        if buf.episodes_in_buffer == case["B"]:
+            ids = np.arange(case["B"])
+        else:
+            ids = np.random.choice(buf.episodes_in_buffer, case["B"], replace=False)
+        np.random.set_state(after)
+        assert np.array_equal(batch["obs"].numpy(), buf["obs"][ids].numpy())
+        ids_all.append(ids.astype(np.int64))
+        max_t = int(batch.max_t_filled())
+        batch = batch[:, :max_t]
+        inter = intermediates(learner, batch)
+        if k < case["record_actions_steps"]:
+            cur_max_steps.append(inter["cur_max_actions"].astype(np.uint8))
+            margin_steps.append(inter["margin"].astype(np.float32))
+        if full and k == 0:
+            for kk, vv in inter.items():
+                out["step0_" + kk] = np.asarray(vv)
+            out["step0_max_t"] = np.array(max_t)
+            # greedy select_actions(test_mode=True) over the whole sampled batch, t = 0..max_t-1
+            # (Categorical(avail) inside select_action raises on an all-zero avail row, so stop at the first
+            #  padded slot of the shortest episode)
+            t_all = int(batch["filled"].sum(1).min())
+            mac.init_hidden(batch.batch_size)
+            acts = [mac.select_actions(batch, t_ep=t, t_env=0, test_mode=True).numpy() for t in range(t_all)]
+            out["greedy_actions"] = np.stack(acts, 1).astype(np.int64)
+        learner.train(batch, t_env=1000 * k, episode_num=episodes[k])
+        losses.append(logger.stats["loss"][-1])
+        assert abs(losses[-1] - inter["loss"]) <= 1e-6 * max(1.0, abs(losses[-1])), (losses[-1], inter["loss"])
+        if full and k == 0:
+            out["step0_grads_clipped"] = flat_grads(learner)
+        if full:
+            per_step["params"].append(flat_params(learner))
+            per_step["targets"].append(flat_targets(learner))
+            per_step["sqavg"].append(flat_sqavg(learner))
+    out["ids"] = np.stack(ids_all)
+    for key in ["loss", "grad_norm", "td_error_abs", "q_taken_mean", "target_mean"]:
+        out["stat_" + key] = np.array(logger.stats[key], dtype=np.float64)
+    if cur_max_steps:
+        out["cur_max_actions"] = np.stack(cur_max_steps)
+        out["margin"] = np.stack(margin_steps)
+    if full:
+        out["step_params"] = np.stack(per_step["params"])
+        out["targets_final"] = per_step["targets"][-1]
+        out["sqavg_final"] = per_step["sqavg"][-1]
+    else:
+        out["params_final"] = flat_params(learner)
+        out["targets_final"] = flat_targets(learner)
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **out)
+    print(name, "steps", case["steps"], "loss[0..]", np.round(out["stat_loss"][:4], 6), "->", path,
+          os.path.getsize(path) // 1024, "KB")
+
+
+TINY = dict(n=3, A=9, O=30, S=48, T=10, B=4, n_episodes=6, data_seed=0, weight_seed=1, sampler_seed=2,
+            ragged=True, steps=4, episodes=[0, 8, 200, 208], full=True, record_actions_steps=4)
+CFG2 = dict(n=8, A=14, O=80, S=168, T=120, B=32, n_episodes=64, data_seed=0, weight_seed=1, sampler_seed=2,
+            ragged=False, steps=20, episodes=[8 * k for k in range(10)] + [200 + 8 * k for k in range(10)],
+            full=False, record_actions_steps=3)
+
+CASES = {
+    "tiny_qmix": dict(TINY, mixer="qmix"),
+    "tiny_vdn": dict(TINY, mixer="vdn"),
+    "tiny_qmix_full": dict(TINY, mixer="qmix", ragged=False, n_episodes=4, steps=3, episodes=[0, 200, 201]),
+    "cfg2_qmix": dict(CFG2, mixer="qmix"),
+    "cfg2_vdn": dict(CFG2, mixer="vdn", steps=10, episodes=[8 * k for k in range(5)] + [200 + k for k in range(5)]),
+    "cfg2_qmix_ragged": dict(CFG2, mixer="qmix", ragged=True, steps=5, episodes=[0, 8, 200, 208, 216]),
+}
+
+if __name__ == "__main__":
+    only = sys.argv[1:]
+    for name, case in CASES.items():
+        if only and name not in only:
+            continue
+        run_case(name, case)

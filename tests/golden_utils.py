@@ -1,0 +1,60 @@
+"""Helpers shared by the parity tests: load a golden case, rebuild its replay and weights bit-exactly."""
+from __future__ import annotations
+
+import os
+from collections import OrderedDict
+
+import numpy as np
+
+from pymarl_amd.utils.synthetic import agent_param_shapes, init_params, make_replay, qmix_param_shapes
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASE_NAMES = ["tiny_qmix", "tiny_vdn", "tiny_qmix_full", "cfg2_qmix", "cfg2_vdn", "cfg2_qmix_ragged"]
+
+
+class Case:
+    def __init__(self, name):
+        self.name = name
+        z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+        self.z = {k: z[k] for k in z.files}
+        g = lambda k: int(self.z[k])  # noqa: E731
+        self.n, self.A, self.O, self.S, self.T = g("n"), g("A"), g("O"), g("S"), g("T")
+        self.B, self.n_episodes, self.steps = g("B"), g("n_episodes"), g("steps")
+        self.mixer = str(self.z["mixer"])
+        self.ragged = bool(self.z["ragged"])
+        self.episodes = [int(e) for e in self.z["episodes"]]
+        self.data = make_replay(self.n_episodes, self.T, self.n, self.A, self.O, self.S,
+                                seed=g("data_seed"), ragged=self.ragged)
+        self.I = self.O + self.A + self.n
+        self.agent_shapes = agent_param_shapes(self.I, 64, self.A)
+        self.mixer_shapes = qmix_param_shapes(self.S, self.n, 32) if self.mixer == "qmix" else OrderedDict()
+        self.agent_params = init_params(self.agent_shapes, seed=g("weight_seed"))
+        self.mixer_params = (init_params(self.mixer_shapes, seed=g("weight_seed") + 100)
+                             if self.mixer == "qmix" else OrderedDict())
+        self.sampler_seed = g("sampler_seed")
+
+    def cfg(self):
+        return dict(n_agents=self.n, n_actions=self.A, obs_dim=self.O, state_dim=self.S, mixer=self.mixer,
+                    gamma=0.99, lr=5e-4, optim_alpha=0.99, optim_eps=1e-5, grad_norm_clip=10.0, double_q=True,
+                    target_update_interval=200, learner_log_interval=0, rnn_hidden_dim=64, mixing_embed_dim=32)
+
+    def batch(self, step):
+        """The (ids-gathered, max_t-truncated) numpy batch the reference trained on at `step`."""
+        ids = self.z["ids"][step]
+        b = OrderedDict((k, v[ids]) for k, v in self.data.items())
+        max_t = int(b["filled"].sum(1).max())
+        return OrderedDict((k, v[:, :max_t]) for k, v in b.items()), ids
+
+    def unflatten(self, flat):
+        out, o = OrderedDict(), 0
+        for k, s in list(self.agent_shapes.items()) + list(self.mixer_shapes.items()):
+            sz = int(np.prod(s))
+            out[k] = flat[o:o + sz].reshape(s)
+            o += sz
+        return out
+
+
+def rel_err(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(1e-30, np.abs(b).max()))
