@@ -1,0 +1,147 @@
+"""ctypes binding of libmq_learner.so (the C ABI declared in include/mq_learner.h).
+
+The product path has no fallback: if the library is missing, or the device is not a HIP GPU, the learner fails
+loudly here. Build it with `python __graft_entry__.py build` (or `make -C pymarl_amd/csrc`).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MQ_LEARNER_LIB", os.path.join(HERE, "lib", "libmq_learner.so"))
+
+MIXER_NONE, MIXER_VDN, MIXER_QMIX = 0, 1, 2
+NSUMS = 8
+NSTATS = 8
+PARAM_NAMES = [
+    "fc1.weight", "fc1.bias", "rnn.weight_ih", "rnn.weight_hh", "rnn.bias_ih", "rnn.bias_hh", "fc2.weight",
+    "fc2.bias", "hyper_w_1.weight", "hyper_w_1.bias", "hyper_w_final.weight", "hyper_w_final.bias",
+    "hyper_b_1.weight", "hyper_b_1.bias", "V.0.weight", "V.0.bias", "V.2.weight", "V.2.bias",
+]
+P_COUNT = len(PARAM_NAMES)
+
+# Every symbol include/mq_learner.h declares (checked by tests/test_boundary.py).
+EXPORTS = [
+    "mq_last_error", "mq_create", "mq_destroy", "mq_param_offsets", "mq_bind", "mq_forward_backward", "mq_apply",
+    "mq_train_step", "mq_update_targets", "mq_copy_intermediate", "mq_mac_forward", "mq_agent_forward",
+    "mq_greedy_actions", "mq_set_timing", "mq_phase_times", "mq_phase_names",
+]
+
+
+class MQConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_agents", ctypes.c_int32), ("n_actions", ctypes.c_int32), ("obs_dim", ctypes.c_int32),
+        ("state_dim", ctypes.c_int32), ("rnn_hidden_dim", ctypes.c_int32), ("mixing_embed_dim", ctypes.c_int32),
+        ("mixer", ctypes.c_int32), ("double_q", ctypes.c_int32), ("obs_last_action", ctypes.c_int32),
+        ("obs_agent_id", ctypes.c_int32), ("gamma", ctypes.c_float), ("lr", ctypes.c_float),
+        ("optim_alpha", ctypes.c_float), ("optim_eps", ctypes.c_float), ("grad_norm_clip", ctypes.c_float),
+        ("max_batch", ctypes.c_int32), ("max_seq", ctypes.c_int32),
+    ]
+
+
+class MQReplay(ctypes.Structure):
+    _fields_ = [
+        ("obs", ctypes.c_void_p), ("state", ctypes.c_void_p), ("actions", ctypes.c_void_p),
+        ("avail_actions", ctypes.c_void_p), ("reward", ctypes.c_void_p), ("terminated", ctypes.c_void_p),
+        ("filled", ctypes.c_void_p), ("ep_ids", ctypes.c_void_p), ("n_episodes", ctypes.c_int64),
+        ("batch_size", ctypes.c_int32), ("t_len", ctypes.c_int32), ("t_stride", ctypes.c_int32),
+    ]
+
+
+_LIB = None
+
+
+class MQError(RuntimeError):
+    pass
+
+
+def load(required=True):
+    """Load the shared library once; raise MQError (no fallback) if it cannot be loaded."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        if not required:
+            return None
+        raise MQError(f"libmq_learner.so not found at {LIB_PATH}; build it with `python __graft_entry__.py build`")
+    import torch  # noqa: F401  (loads torch's HIP runtime first so the library binds to the same one)
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    sig = {
+        "mq_last_error": ([], ctypes.c_char_p),
+        "mq_phase_names": ([], ctypes.c_char_p),
+        "mq_create": ([ctypes.POINTER(MQConfig), ctypes.POINTER(vp)], ctypes.c_int),
+        "mq_destroy": ([vp], ctypes.c_int),
+        "mq_param_offsets": ([vp, ctypes.POINTER(i64)], ctypes.c_int),
+        "mq_bind": ([vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
+        "mq_forward_backward": ([vp, ctypes.POINTER(MQReplay), vp], ctypes.c_int),
+        "mq_apply": ([vp, vp], ctypes.c_int),
+        "mq_train_step": ([vp, ctypes.POINTER(MQReplay), vp], ctypes.c_int),
+        "mq_update_targets": ([vp, vp], ctypes.c_int),
+        "mq_copy_intermediate": ([vp, ctypes.c_int, vp, ctypes.POINTER(i64), vp], ctypes.c_int),
+        "mq_mac_forward": ([vp, ctypes.POINTER(MQReplay), i32, vp, vp, vp, i32, vp], ctypes.c_int),
+        "mq_agent_forward": ([vp, vp, i32, vp, vp, vp, i32, vp], ctypes.c_int),
+        "mq_greedy_actions": ([vp, vp, vp, i32, i32, vp], ctypes.c_int),
+        "mq_set_timing": ([vp, i32], ctypes.c_int),
+        "mq_phase_times": ([vp, ctypes.POINTER(ctypes.c_float), i32, ctypes.POINTER(i32)], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _LIB = lib
+    return lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = _LIB.mq_last_error().decode() if _LIB is not None else "library not loaded"
+        if "not recognised" in msg:
+            raise ValueError(msg)
+        raise MQError(f"libmq_learner error {rc}: {msg}")
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (None -> NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_gpu(tensor_or_device):
+    import torch
+    dev = getattr(tensor_or_device, "device", tensor_or_device)
+    dev = torch.device(dev)
+    if dev.type != "cuda" or not torch.cuda.is_available():
+        raise MQError(f"the MI355X learner path needs HIP device tensors (got device {dev}); there is no CPU "
+                      "fallback — call .cuda() on the learner/MAC and keep the replay on the GPU")
+
+
+class Handle:
+    """RAII owner of an mq_handle."""
+
+    def __init__(self, cfg: MQConfig):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        check(self.lib.mq_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+        self.cfg = cfg
+        offs = (ctypes.c_int64 * (P_COUNT + 1))()
+        check(self.lib.mq_param_offsets(self.h, offs))
+        self.offsets = list(offs)
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) and self.h.value:
+                self.lib.mq_destroy(self.h)
+                self.h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+    @property
+    def n_params(self):
+        return self.offsets[-1]

@@ -1,0 +1,79 @@
+"""BasicMAC: parameter-shared multi-agent controller (reference: src/controllers/basic_controller.py:10-154).
+
+`forward(ep_batch, t)` is one fused HIP step (`mq_mac_forward`): it builds [obs_t | onehot(a_{t-1}) | onehot(id)]
+from the replay rows in-kernel (basic_controller.py:100-135) and runs fc1 -> GRUCell -> fc2 for every
+(episode, agent) row. Only the "q" agent_output_type (QMIX/VDN/IQL) is implemented.
+"""
+import torch as th
+
+from .. import _lib
+from ..components.action_selectors import REGISTRY as action_REGISTRY
+from ..modules.agents import REGISTRY as agent_REGISTRY
+
+
+class BasicMAC:
+    def __init__(self, scheme, groups, args):
+        self.n_agents = args.n_agents
+        self.args = args
+        input_shape = self._get_input_shape(scheme)
+        self._build_agents(input_shape)
+        self.agent_output_type = args.agent_output_type
+        self.action_selector = action_REGISTRY[args.action_selector](args)
+        self.hidden_states = None
+
+    def select_actions(self, ep_batch, t_ep, t_env, bs=slice(None), test_mode=False):
+        avail_actions = ep_batch["avail_actions"][:, t_ep]
+        agent_outputs = self.forward(ep_batch, t_ep, test_mode=test_mode)
+        return self.action_selector.select_action(agent_outputs[bs], avail_actions[bs], t_env, test_mode=test_mode)
+
+    def forward(self, ep_batch, t, test_mode=False):
+        if self.agent_output_type != "q":
+            raise NotImplementedError("agent_output_type {!r}: only 'q' is implemented".format(self.agent_output_type))
+        from ..learners.q_learner import replay_view
+        rep, keep = replay_view(ep_batch)
+        bs = ep_batch.batch_size
+        H = self.args.rnn_hidden_dim
+        h_in = self.hidden_states.reshape(bs * self.n_agents, H).float().contiguous()
+        _lib.require_gpu(h_in)
+        h_out = th.empty_like(h_in)
+        q = th.empty(bs * self.n_agents, self.args.n_actions, dtype=th.float32, device=h_in.device)
+        hd = self.agent.handle()
+        _lib.check(hd.lib.mq_mac_forward(hd.h, rep, int(t), _lib.ptr(h_in), _lib.ptr(h_out), _lib.ptr(q), 0,
+                                         _lib.stream_ptr()))
+        self.hidden_states = h_out.view(bs, self.n_agents, H)
+        return q.view(bs, self.n_agents, -1)
+
+    def init_hidden(self, batch_size):
+        self.hidden_states = self.agent.init_hidden().unsqueeze(0).expand(batch_size, self.n_agents, -1)
+
+    def parameters(self):
+        return self.agent.parameters()
+
+    def load_state(self, other_mac):
+        self.agent.load_state_dict(other_mac.agent.state_dict())
+
+    def cuda(self):
+        self.agent.cuda()
+
+    def save_models(self, path):
+        th.save(self.agent.state_dict(), "{}/agent.th".format(path))
+
+    def load_models(self, path):
+        self.agent.load_state_dict(th.load("{}/agent.th".format(path), map_location=lambda s, loc: s,
+                                           weights_only=True))
+
+    def _build_agents(self, input_shape):
+        self.agent = agent_REGISTRY[self.args.agent](input_shape, self.args)
+
+    def _get_input_shape(self, scheme):
+        """basic_controller.py:137-154, without mutating `scheme` (the reference's in-place int->tuple rewrite of
+        scheme["obs"]["vshape"] is what breaks COMACritic)."""
+        vs = scheme["obs"]["vshape"]
+        obs = vs if isinstance(vs, int) else int(vs[0])
+        width = obs
+        if self.args.obs_last_action:
+            oh = scheme["actions_onehot"]["vshape"]
+            width += oh if isinstance(oh, int) else int(oh[0])
+        if self.args.obs_agent_id:
+            width += self.n_agents
+        return (width,)

@@ -1,0 +1,59 @@
+// Shared device helpers for the MI355X (gfx950) QMIX/VDN learner kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MQ_DEV __device__ __forceinline__
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace mq {
+
+constexpr float kNegMask = -9999999.0f;   // q_learner.py:68,74
+
+// Unsigned 32-bit division by a runtime-invariant divisor: q = (umulhi(x, mul) + x) >> shift, valid for
+// x < 2^31 (row/step indices here are far below that). Host computes (mul, shift) once per launch.
+struct FastDiv {
+  uint32_t d, mul, shift;
+};
+
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.shift = l;
+  f.mul = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+  if (d == 1) { f.mul = 0; f.shift = 0; }
+  return f;
+}
+
+MQ_DEV uint32_t fdiv(uint32_t x, const FastDiv& f) {
+  uint32_t t = __umulhi(x, f.mul);
+  return (t + x) >> f.shift;
+}
+
+// Lane exchange inside an aligned group of 4 lanes (DPP quad_perm, no LDS round trip).
+MQ_DEV float quad_xor1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
+}
+MQ_DEV float quad_xor2(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
+}
+// Sum over the 4 lanes of a quad; every lane of the quad receives the same total ((a+b)+(c+d) order).
+MQ_DEV float quad_sum(float v) {
+  v = v + quad_xor1(v);
+  return v + quad_xor2(v);
+}
+
+MQ_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+MQ_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+MQ_DEV float tanhf_(float x) { return tanhf(x); }
+
+}  // namespace mq

@@ -1,0 +1,66 @@
+// Shapes, replay view and workspace of one learner train step (shared by every kernel of the step).
+#pragma once
+#include "common.hpp"
+#include "../../include/mq_learner.h"
+
+namespace mq {
+
+constexpr int H = 64;        // rnn_hidden_dim (reference default, rnn_agent.py:19-21)
+constexpr int G3 = 3 * H;    // GRU gate width (r, z, n)
+
+struct Dims {
+  int n, A, O, S, E, I, NH;  // agents, actions, obs, state, mixer embed, agent input width, hypernet outputs
+  int B, Tp, T, R, M;        // episodes, unrolled steps (max_t_filled), transitions, rows B*n, mixer rows T*B
+  int t_stride;              // storage max_seq_length
+  int last_action, agent_id, mixer, double_q;
+  float gamma;
+  FastDiv dR, dN, dB;
+  MQ_DEV int64_t RT() const { return (int64_t)Tp * R; }
+};
+
+// Borrowed replay storage (reference scheme dtypes), episode-major, plus the sampled episode ids.
+struct Rep {
+  const float* obs;
+  const float* state;
+  const int64_t* actions;
+  const int32_t* avail;
+  const float* reward;
+  const uint8_t* term;
+  const int64_t* filled;
+  const int64_t* ep_ids;
+  MQ_DEV int64_t ep(int b) const { return ep_ids ? ep_ids[b] : (int64_t)b; }
+};
+
+struct Lay {
+  int64_t o[MQ_P_COUNT + 1];
+};
+
+// Activation workspace, time-major: row index tr = t*R + r with r = b*n + agent.
+struct Work {
+  float* X1;      // [2][RT][H]   relu(fc1) per net
+  float* GI;      // [2][RT][3H]  W_ih x1 + b_ih per net
+  float* Hs;      // [RT][H]      online hidden after step t
+  float* Gates;   // [RT][4H]     online r, z, n, W_hn h + b_hn
+  float* Q;       // [2][RT][A]   mac_out / target_mac_out
+  float* HYP;     // [2][M][NH]   QMIX hypernet outputs per net (state t for online, t+1 for target)
+  float* dHYP;    // [M][NH]
+  float* dch;     // [T*R]        dLoss_num/dchosen
+  float* dGI;     // [RT][3H]
+  float* dP1;     // [RT][H]
+  float* slab_fc1;   // [nsplit][H*I + H]
+  float* slab_rnn;   // [blocks][len_rnn]   w_ih, w_hh, b_ih, b_hh, fc2.w, fc2.b
+  float* slab_mix;   // [nsplit][len_mix]   hyper_w_1 .. V.0 (weights+biases)
+  float* slab_v2;    // [mix blocks][E+1]   V.2 weight, bias
+  float* loss_part;  // [mix blocks][8]
+  float* norm_part;  // [norm blocks]
+  int32_t* curmax;   // [T*R]
+};
+
+MQ_DEV void split_tr(const Dims& d, uint32_t tr, int& t, int& r, int& b, int& ag) {
+  t = (int)fdiv(tr, d.dR);
+  r = (int)tr - t * d.R;
+  b = (int)fdiv((uint32_t)r, d.dN);
+  ag = r - b * d.n;
+}
+
+}  // namespace mq

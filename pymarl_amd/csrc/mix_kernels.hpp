@@ -1,0 +1,188 @@
+// Per-(episode, t) tail of QLearner.train: chosen-action gather, double-Q target selection, QMIX / VDN mixing
+// (forward for both nets), 1-step TD target, masked L2 terms, the learner stats sums, and the mixer backward
+// down to dLoss/dchosen (q_learner.py:39-97; qmix.py:28-47; vdn.py:9-10).
+//
+// One wave per (t, b) pair m = t*B + b; 4 pairs per 256-thread workgroup. Lanes play agents for the
+// selection (argmax over available actions, first index on ties as torch max) and embedding units for the
+// mixer; the few cross-lane sums are wave reductions. Loss sums stay UNNORMALISED (sum (td*m)^2 etc.) so a
+// data-parallel all-reduce of them reproduces the reference's global / sum(mask) exactly.
+#pragma once
+#include "learner_types.hpp"
+
+namespace mq {
+
+MQ_DEV float sgnf(float x) { return (float)((x > 0.0f) - (x < 0.0f)); }
+MQ_DEV float eluf(float x) { return x > 0.0f ? x : expm1f(x); }
+
+struct MixOut {
+  float y, pre, hid, wf_raw, hv;   // lane-e intermediates of the online mixer (QMIX)
+};
+
+// QMIX forward for one (t, b): lanes e < E. Returns y (same on every lane).
+MQ_DEV float qmix_fwd_lane(const float* hyp, const float* qs_lds, const float* V2w, float V2b, int n, int E,
+                           int lane, MixOut* keep) {
+  const int nE = n * E;
+  float prod = 0.0f, vt = 0.0f, pre = 0.0f, hid = 0.0f, wfr = 0.0f, hv = 0.0f;
+  if (lane < E) {
+    float acc = 0.0f;
+    for (int ag = 0; ag < n; ++ag) acc = fmaf(qs_lds[ag], fabsf(hyp[ag * E + lane]), acc);   // bmm(q, |w1|)
+    pre = acc + hyp[nE + E + lane];                                                          // + b1
+    hid = eluf(pre);
+    wfr = hyp[nE + lane];
+    prod = hid * fabsf(wfr);                                                                 // bmm(hid, |wf|)
+    hv = hyp[nE + 2 * E + lane];
+    vt = fmaxf(hv, 0.0f) * V2w[lane];                                                        // V(s)
+  }
+  const float y = wave_sum(prod) + (wave_sum(vt) + V2b);
+  if (keep) { keep->y = y; keep->pre = pre; keep->hid = hid; keep->wf_raw = wfr; keep->hv = hv; }
+  return y;
+}
+
+__global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* __restrict__ P0,
+                                                  const float* __restrict__ P1, Lay L, Work w, int32_t* curmax_out) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + wv;
+  const int n = d.n, A = d.A, E = d.E, R = d.R, NH = d.NH;
+  __shared__ float chs[4][64], tms[4][64], dps[4][64];
+  __shared__ float red[4][8];
+  __shared__ float v2red[4][65];
+  float l2 = 0.0f, msk = 0.0f, abs_ = 0.0f, qs = 0.0f, tg = 0.0f;   // lane-0 partials of this wave
+  float dv2 = 0.0f, dv2b = 0.0f;
+  const bool valid = m < d.M;
+  int t = 0, b = 0;
+  int64_t ep = 0;
+  if (valid) {
+    t = (int)fdiv((uint32_t)m, d.dB);
+    b = m - t * d.B;
+    ep = rp.ep(b);
+  }
+  const float* Qon = w.Q;
+  const float* Qtg = w.Q + d.RT() * A;
+  // ---- chosen action values and double-Q target selection (q_learner.py:55, 68-78); lane = agent
+  float chosen = 0.0f, tmax = 0.0f;
+  if (valid && lane < n) {
+    const int r = b * n + lane;
+    const int64_t slot = ep * d.t_stride + t;
+    const int at = (int)rp.actions[slot * n + lane];
+    chosen = Qon[((int64_t)t * R + r) * A + at];
+    const float* qn = Qon + ((int64_t)(t + 1) * R + r) * A;
+    const float* qt = Qtg + ((int64_t)(t + 1) * R + r) * A;
+    const int32_t* av = rp.avail + ((slot + 1) * n + lane) * (int64_t)A;
+    int cur = 0;
+    if (d.double_q) {
+      float best = 0.0f;
+      for (int a = 0; a < A; ++a) {
+        const float v = av[a] ? qn[a] : kNegMask;
+        if (a == 0 || v > best) { best = v; cur = a; }
+      }
+      tmax = av[cur] ? qt[cur] : kNegMask;
+    } else {
+      float best = 0.0f;
+      for (int a = 0; a < A; ++a) {
+        const float v = av[a] ? qt[a] : kNegMask;
+        if (a == 0 || v > best) { best = v; cur = a; }
+      }
+      tmax = best;
+    }
+    if (curmax_out) curmax_out[(int64_t)t * R + r] = cur;
+  }
+  chs[wv][lane] = chosen;
+  tms[wv][lane] = tmax;
+  __syncthreads();
+
+  float mask = 0.0f, rew = 0.0f, term = 0.0f;
+  if (valid) {
+    const int64_t slot = ep * d.t_stride + t;
+    mask = (float)rp.filled[slot];
+    if (t > 0) mask *= 1.0f - (float)rp.term[slot - 1];   // q_learner.py:42-43
+    rew = rp.reward[slot];
+    term = (float)rp.term[slot];
+  }
+  const float gamma = d.gamma;
+  if (d.mixer == MQ_MIXER_QMIX) {
+    const float* hon = w.HYP + (int64_t)m * NH;
+    const float* htg = w.HYP + ((int64_t)d.M + m) * NH;
+    const float* V2w0 = P0 + L.o[MQ_P_V2_W];
+    const float* V2w1 = P1 + L.o[MQ_P_V2_W];
+    MixOut k;
+    float y = 0.0f, yt = 0.0f;
+    if (valid) {
+      y = qmix_fwd_lane(hon, chs[wv], V2w0, P0[L.o[MQ_P_V2_B]], n, E, lane, &k);
+      yt = qmix_fwd_lane(htg, tms[wv], V2w1, P1[L.o[MQ_P_V2_B]], n, E, lane, nullptr);
+    } else {
+      k.y = k.pre = k.hid = k.wf_raw = k.hv = 0.0f;
+    }
+    const float target = rew + gamma * (1.0f - term) * yt;   // q_learner.py:86
+    const float td = y - target;
+    const float mtd = td * mask;
+    l2 = mtd * mtd; msk = mask; abs_ = fabsf(mtd); qs = y * mask; tg = target * mask;
+    const float dy = (2.0f * mtd) * mask;                     // d sum (td*m)^2 / d Q_tot
+    // ---- QMIX backward (lanes e < E)
+    float dpre = 0.0f;
+    if (valid && lane < E) {
+      const float wf = fabsf(k.wf_raw);
+      const float dhid = dy * wf;
+      float* dh = w.dHYP + (int64_t)m * NH;
+      dh[n * E + lane] = dy * k.hid * sgnf(k.wf_raw);                         // hyper_w_final
+      dpre = dhid * (k.pre > 0.0f ? 1.0f : expf(k.pre));                      // elu'
+      dh[n * E + E + lane] = dpre;                                            // hyper_b_1
+      dh[n * E + 2 * E + lane] = dy * V2w0[lane] * (k.hv > 0.0f ? 1.0f : 0.0f);   // V.0 (through relu)
+      dv2 = dy * fmaxf(k.hv, 0.0f);                                           // V.2 weight
+      for (int ag = 0; ag < n; ++ag)                                          // hyper_w_1 (through |.|)
+        dh[ag * E + lane] = (chs[wv][ag] * dpre) * sgnf(hon[ag * E + lane]);
+    }
+    dv2b = dy;
+    dps[wv][lane] = dpre;
+    __syncthreads();
+    if (valid && lane < n) {
+      float acc = 0.0f;
+      for (int e = 0; e < E; ++e) acc = fmaf(fabsf(hon[lane * E + e]), dps[wv][e], acc);
+      w.dch[(int64_t)t * R + b * n + lane] = acc;
+    }
+  } else {
+    float y, yt;
+    if (d.mixer == MQ_MIXER_VDN) {
+      y = wave_sum(lane < n ? chosen : 0.0f);
+      yt = wave_sum(lane < n ? tmax : 0.0f);
+    } else {   // no mixer: per-agent TD (q_learner.py:81 skipped; mask expanded over agents)
+      y = chosen;
+      yt = tmax;
+    }
+    const float target = rew + gamma * (1.0f - term) * yt;
+    const float td = y - target;
+    const float mtd = td * mask;
+    const float dy = (2.0f * mtd) * mask;
+    if (d.mixer == MQ_MIXER_VDN) {
+      l2 = mtd * mtd; msk = mask; abs_ = fabsf(mtd); qs = y * mask; tg = target * mask;
+    } else {
+      const bool on = lane < n;
+      l2 = wave_sum(on ? mtd * mtd : 0.0f);
+      msk = wave_sum(on ? mask : 0.0f);
+      abs_ = wave_sum(on ? fabsf(mtd) : 0.0f);
+      qs = wave_sum(on ? y * mask : 0.0f);
+      tg = wave_sum(on ? target * mask : 0.0f);
+    }
+    if (valid && lane < n) w.dch[(int64_t)t * R + b * n + lane] = dy;
+    __syncthreads();   // match the QMIX branch's barrier count
+  }
+  if (!valid) { l2 = msk = abs_ = qs = tg = 0.0f; dv2 = dv2b = 0.0f; }
+  // ---- deterministic per-workgroup partials
+  if (lane == 0) {
+    red[wv][0] = l2; red[wv][1] = msk; red[wv][2] = abs_; red[wv][3] = qs; red[wv][4] = tg;
+    v2red[wv][64] = dv2b;
+  }
+  v2red[wv][lane] = dv2;
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    const int c = threadIdx.x;
+    float* out = w.loss_part + (int64_t)blockIdx.x * 8;
+    out[c] = c < 5 ? ((red[0][c] + red[1][c]) + (red[2][c] + red[3][c])) : 0.0f;
+  }
+  if (d.mixer == MQ_MIXER_QMIX && threadIdx.x <= E) {
+    const int e = threadIdx.x == E ? 64 : threadIdx.x;
+    w.slab_v2[(int64_t)blockIdx.x * (E + 1) + threadIdx.x] =
+        (v2red[0][e] + v2red[1][e]) + (v2red[2][e] + v2red[3][e]);
+  }
+}
+
+}  // namespace mq

@@ -1,0 +1,519 @@
+// libmq_learner: MI355X-native QMIX/VDN learner step behind the C ABI of include/mq_learner.h.
+//
+// One train step (QLearner.train, q_learner.py:37-116) is this stream-ordered launch sequence:
+//   fc1      gemm  X1 = relu(W1 [obs | a_{t-1} | id] + b1)               both nets, rows gathered by episode id
+//   gi       gemm  GI = W_ih X1 + b_ih                                    both nets
+//   gru_fwd  recur h_t = GRU(GI_t, h_{t-1}); q_t = W2 h_t + b2           both nets, serial over T
+//   hyper    gemm  QMIX hypernet outputs of state[:, :-1] / state[:, 1:] both nets (QMIX only)
+//   mix      per (t, episode): chosen gather, double-Q select, mixer fwd, TD, masked L2 sums, mixer bwd
+//   gru_bwd  recur BPTT; dW_hh, dW_ih, dW2 and biases accumulated in-kernel, dGI written out
+//   dx1      gemm  dP1 = (dGI W_ih) * [X1 > 0]
+//   dw1      gemm  [dW1 | db1] = dP1^T xin                                split-K
+//   dwh      gemm  [dW_hyper | db_hyper] = dHYP^T state                   split-K (QMIX only)
+//   reduce   deterministic slab sums -> flat gradient buffer (+ loss sums)
+//   --- (data-parallel all-reduce of the gradient buffer happens here, in the caller)
+//   norm     partial sum of squares
+//   apply    / sum(mask), clip_grad_norm_, RMSprop
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "learner_gemms.hpp"
+#include "gru_kernels.hpp"
+#include "mix_kernels.hpp"
+#include "optim_kernels.hpp"
+
+using namespace mq;
+
+namespace {
+
+std::mutex g_err_mu;
+std::string g_err;
+
+int set_err(int code, const std::string& msg) {
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  g_err = msg;
+  return code;
+}
+
+#define MQ_HIP(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess)                                                                   \
+      return set_err(MQ_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));        \
+  } while (0)
+
+constexpr int kNsplitMax = 128;
+constexpr int kNormBlocks = 256;
+enum Phase { PH_FC1, PH_GI, PH_GRUF, PH_HYP, PH_MIX, PH_GRUB, PH_DX1, PH_DW1, PH_DWH, PH_RED, PH_NORM,
+             PH_APPLY, PH_N };
+const char* kPhaseNames = "fc1;gi;gru_fwd;hyper;mix;gru_bwd;dx1;dw1;dwh;reduce;norm;apply";
+
+int pick_rw(int R, int max_blocks) {
+  const int rws[4] = {1, 2, 4, 8};
+  for (int i = 0; i < 4; ++i)
+    if ((R + rws[i] - 1) / rws[i] <= max_blocks) return rws[i];
+  return 8;
+}
+
+}  // namespace
+
+struct mq_handle {
+  mq_config cfg;
+  int I, E, NH;
+  int64_t off[MQ_P_COUNT + 1];
+  int64_t P;
+  int64_t len_rnn, len_mix;
+  // bound (caller-owned)
+  float *on = nullptr, *tg = nullptr, *grad = nullptr, *sq = nullptr, *stats = nullptr;
+  int32_t* curmax_user = nullptr;
+  // workspace (handle-owned)
+  void* ws = nullptr;
+  Work w;
+  int32_t* curmax_ws = nullptr;
+  // last step bookkeeping
+  bool have_fb = false;
+  Dims last;
+  int nsplit_fc1 = 1, nsplit_mix = 1, nblk_bwd = 1, nblk_mix = 1;
+  // timing
+  bool timing = false;
+  hipEvent_t ev0[PH_N], ev1[PH_N];
+  bool ev_used[PH_N];
+  bool ev_made = false;
+};
+
+namespace {
+
+void compute_layout(mq_handle* h) {
+  const mq_config& c = h->cfg;
+  const int Hd = mq::H, n = c.n_agents, A = c.n_actions, S = c.state_dim, E = h->E, I = h->I;
+  int64_t sz[MQ_P_COUNT] = {};
+  sz[MQ_P_FC1_W] = (int64_t)Hd * I; sz[MQ_P_FC1_B] = Hd;
+  sz[MQ_P_RNN_W_IH] = 3LL * Hd * Hd; sz[MQ_P_RNN_W_HH] = 3LL * Hd * Hd;
+  sz[MQ_P_RNN_B_IH] = 3 * Hd; sz[MQ_P_RNN_B_HH] = 3 * Hd;
+  sz[MQ_P_FC2_W] = (int64_t)A * Hd; sz[MQ_P_FC2_B] = A;
+  if (c.mixer == MQ_MIXER_QMIX) {
+    sz[MQ_P_HW1_W] = (int64_t)E * n * S; sz[MQ_P_HW1_B] = (int64_t)E * n;
+    sz[MQ_P_HWF_W] = (int64_t)E * S; sz[MQ_P_HWF_B] = E;
+    sz[MQ_P_HB1_W] = (int64_t)E * S; sz[MQ_P_HB1_B] = E;
+    sz[MQ_P_V0_W] = (int64_t)E * S; sz[MQ_P_V0_B] = E;
+    sz[MQ_P_V2_W] = E; sz[MQ_P_V2_B] = 1;
+  }
+  int64_t o = 0;
+  for (int i = 0; i < MQ_P_COUNT; ++i) { h->off[i] = o; o += sz[i]; }
+  h->off[MQ_P_COUNT] = o;
+  h->P = o;
+  h->len_rnn = h->off[MQ_P_FC2_B] + A - h->off[MQ_P_RNN_W_IH];
+  h->len_mix = h->off[MQ_P_V2_W] - h->off[MQ_P_HW1_W];
+}
+
+int64_t align_up(int64_t x) { return (x + 63) & ~int64_t(63); }
+
+Dims make_dims(const mq_handle* h, const mq_replay* b) {
+  const mq_config& c = h->cfg;
+  Dims d;
+  d.n = c.n_agents; d.A = c.n_actions; d.O = c.obs_dim; d.S = c.state_dim; d.E = h->E; d.I = h->I; d.NH = h->NH;
+  d.B = b->batch_size; d.Tp = b->t_len; d.T = b->t_len - 1; d.R = d.B * d.n; d.M = d.T * d.B;
+  d.t_stride = b->t_stride;
+  d.last_action = c.obs_last_action; d.agent_id = c.obs_agent_id; d.mixer = c.mixer; d.double_q = c.double_q;
+  d.gamma = c.gamma;
+  d.dR = make_fastdiv((uint32_t)d.R);
+  d.dN = make_fastdiv((uint32_t)d.n);
+  d.dB = make_fastdiv((uint32_t)d.B);
+  return d;
+}
+
+Rep make_rep(const mq_replay* b) {
+  Rep r;
+  r.obs = b->obs; r.state = b->state; r.actions = b->actions; r.avail = b->avail_actions; r.reward = b->reward;
+  r.term = b->terminated; r.filled = b->filled; r.ep_ids = b->ep_ids;
+  return r;
+}
+
+Lay make_lay(const mq_handle* h) {
+  Lay L;
+  for (int i = 0; i <= MQ_P_COUNT; ++i) L.o[i] = h->off[i];
+  return L;
+}
+
+int check_batch(const mq_handle* h, const mq_replay* b) {
+  if (!b) return set_err(MQ_ERR_ARG, "batch is NULL");
+  if (!b->obs || !b->actions || !b->avail_actions || !b->reward || !b->terminated || !b->filled)
+    return set_err(MQ_ERR_ARG, "batch is missing a required field pointer");
+  if (h->cfg.mixer == MQ_MIXER_QMIX && !b->state) return set_err(MQ_ERR_ARG, "QMIX needs batch.state");
+  if (b->batch_size < 1 || b->batch_size > h->cfg.max_batch)
+    return set_err(MQ_ERR_ARG, "batch_size " + std::to_string(b->batch_size) + " outside [1, max_batch=" +
+                                   std::to_string(h->cfg.max_batch) + "]");
+  if (b->t_len < 2 || b->t_len > h->cfg.max_seq || b->t_len > b->t_stride)
+    return set_err(MQ_ERR_ARG, "t_len " + std::to_string(b->t_len) + " must be in [2, min(max_seq, t_stride)]");
+  if ((int64_t)b->t_len * b->batch_size * h->cfg.n_agents >= (1LL << 31))
+    return set_err(MQ_ERR_ARG, "batch too large for 32-bit row indices");
+  return MQ_OK;
+}
+
+struct PhaseTimer {
+  mq_handle* h;
+  hipStream_t s;
+  int cur = -1;
+  void begin(int p) {
+    if (!h->timing) return;
+    end();
+    (void)hipEventRecord(h->ev0[p], s);
+    h->ev_used[p] = true;
+    cur = p;
+  }
+  void end() {
+    if (!h->timing || cur < 0) return;
+    (void)hipEventRecord(h->ev1[cur], s);
+    cur = -1;
+  }
+};
+
+template <int RW>
+hipError_t launch_gru_fwd(const Dims& d, const mq_handle* h, const Lay& L, const Work& w, hipStream_t s) {
+  dim3 grid((d.R + RW - 1) / RW, 2);
+  hipLaunchKernelGGL(gru_fwd_kernel<RW>, grid, dim3(256), 0, s, d, (const float*)h->on, (const float*)h->tg, L, w);
+  return hipGetLastError();
+}
+
+template <int RW>
+hipError_t launch_gru_bwd(const Dims& d, const Rep& rp, const mq_handle* h, const Lay& L, const Work& w,
+                          hipStream_t s, int* nblk) {
+  *nblk = (d.R + RW - 1) / RW;
+  const size_t dyn = ((size_t)d.A * mq::H + d.A) * sizeof(float);
+  hipLaunchKernelGGL(gru_bwd_kernel<RW>, dim3(*nblk), dim3(256), dyn, s, d, rp, (const float*)h->on, L, w,
+                     h->len_rnn);
+  return hipGetLastError();
+}
+
+int reduce_into(const float* slab, int nslab, int64_t len, float* dst, hipStream_t s) {
+  if (len <= 0) return MQ_OK;
+  int blocks = (int)std::min<int64_t>((len + 255) / 256, 2048);
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(blocks), dim3(256), 0, s, slab, nslab, len, dst);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mq_last_error(void) {
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  return g_err.c_str();
+}
+
+const char* mq_phase_names(void) { return kPhaseNames; }
+
+int mq_create(const mq_config* cfg, mq_handle** out) {
+  if (!cfg || !out) return set_err(MQ_ERR_ARG, "NULL argument");
+  const mq_config& c = *cfg;
+  if (c.mixer != MQ_MIXER_NONE && c.mixer != MQ_MIXER_VDN && c.mixer != MQ_MIXER_QMIX)
+    return set_err(MQ_ERR_ARG, "Mixer " + std::to_string(c.mixer) + " not recognised.");
+  if (c.rnn_hidden_dim != mq::H) return set_err(MQ_ERR_ARG, "rnn_hidden_dim must be 64");
+  if (c.n_agents < 1 || c.n_agents > 64) return set_err(MQ_ERR_ARG, "n_agents must be in [1, 64]");
+  if (c.n_actions < 1 || c.n_actions > 64) return set_err(MQ_ERR_ARG, "n_actions must be in [1, 64]");
+  if (c.obs_dim < 1 || c.state_dim < 1) return set_err(MQ_ERR_ARG, "obs_dim / state_dim must be positive");
+  if (c.mixer == MQ_MIXER_QMIX && (c.mixing_embed_dim < 1 || c.mixing_embed_dim > 64))
+    return set_err(MQ_ERR_ARG, "mixing_embed_dim must be in [1, 64]");
+  if (c.max_batch < 1 || c.max_seq < 2) return set_err(MQ_ERR_ARG, "max_batch >= 1 and max_seq >= 2 required");
+
+  mq_handle* h = new mq_handle();
+  h->cfg = c;
+  h->E = c.mixer == MQ_MIXER_QMIX ? c.mixing_embed_dim : 0;
+  h->I = c.obs_dim + (c.obs_last_action ? c.n_actions : 0) + (c.obs_agent_id ? c.n_agents : 0);
+  h->NH = h->E * (c.n_agents + 3);
+  compute_layout(h);
+
+  const int64_t n = c.n_agents, A = c.n_actions, Hd = mq::H;
+  const int64_t RT = (int64_t)c.max_seq * c.max_batch * n;
+  const int64_t Mm = (int64_t)(c.max_seq - 1) * c.max_batch;
+  const int64_t Rm = (int64_t)c.max_batch * n;
+  const int64_t nmix = (Mm + 3) / 4;
+  const int64_t NH = h->NH;
+  int64_t sizes[17] = {
+      2 * RT * Hd,                                   // X1
+      2 * RT * 3 * Hd,                               // GI
+      RT * Hd,                                       // Hs
+      RT * 4 * Hd,                                   // Gates
+      2 * RT * A,                                    // Q
+      2 * Mm * NH,                                   // HYP
+      Mm * NH,                                       // dHYP
+      Mm * n,                                        // dch
+      RT * 3 * Hd,                                   // dGI
+      RT * Hd,                                       // dP1
+      (int64_t)kNsplitMax * (Hd * h->I + Hd),        // slab_fc1
+      Rm * h->len_rnn,                               // slab_rnn (RW = 1 worst case)
+      (int64_t)kNsplitMax * h->len_mix,              // slab_mix
+      nmix * (h->E + 1),                             // slab_v2
+      nmix * 8,                                      // loss_part
+      kNormBlocks,                                   // norm_part
+      Mm * n,                                        // curmax (int32)
+  };
+  int64_t total = 0, offs[17];
+  for (int i = 0; i < 17; ++i) { offs[i] = total; total += align_up(std::max<int64_t>(sizes[i], 1)); }
+  hipError_t e = hipMalloc(&h->ws, total * sizeof(float));
+  if (e != hipSuccess) {
+    delete h;
+    return set_err(MQ_ERR_HIP, std::string("workspace hipMalloc(") + std::to_string(total * 4) + " B): " +
+                                   hipGetErrorString(e));
+  }
+  float* base = (float*)h->ws;
+  Work& w = h->w;
+  w.X1 = base + offs[0]; w.GI = base + offs[1]; w.Hs = base + offs[2]; w.Gates = base + offs[3];
+  w.Q = base + offs[4]; w.HYP = base + offs[5]; w.dHYP = base + offs[6]; w.dch = base + offs[7];
+  w.dGI = base + offs[8]; w.dP1 = base + offs[9]; w.slab_fc1 = base + offs[10]; w.slab_rnn = base + offs[11];
+  w.slab_mix = base + offs[12]; w.slab_v2 = base + offs[13]; w.loss_part = base + offs[14];
+  w.norm_part = base + offs[15];
+  h->curmax_ws = (int32_t*)(base + offs[16]);
+  w.curmax = h->curmax_ws;
+  for (int p = 0; p < PH_N; ++p) h->ev_used[p] = false;
+  *out = h;
+  return MQ_OK;
+}
+
+int mq_destroy(mq_handle* h) {
+  if (!h) return MQ_OK;
+  if (h->ev_made)
+    for (int p = 0; p < PH_N; ++p) { (void)hipEventDestroy(h->ev0[p]); (void)hipEventDestroy(h->ev1[p]); }
+  if (h->ws) (void)hipFree(h->ws);
+  delete h;
+  return MQ_OK;
+}
+
+int mq_param_offsets(const mq_handle* h, int64_t* offsets) {
+  if (!h || !offsets) return set_err(MQ_ERR_ARG, "NULL argument");
+  for (int i = 0; i <= MQ_P_COUNT; ++i) offsets[i] = h->off[i];
+  return MQ_OK;
+}
+
+int mq_bind(mq_handle* h, float* online, float* target, float* grad, float* sq_avg, float* stats,
+            int32_t* cur_max) {
+  // target/grad/sq_avg/stats may be NULL for an inference-only handle (mq_mac_forward / mq_agent_forward)
+  if (!h || !online) return set_err(MQ_ERR_ARG, "NULL handle or online parameters in mq_bind");
+  h->on = online; h->tg = target; h->grad = grad; h->sq = sq_avg; h->stats = stats; h->curmax_user = cur_max;
+  return MQ_OK;
+}
+
+int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
+  if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
+  if (!h->on || !h->tg || !h->grad || !h->sq || !h->stats)
+    return set_err(MQ_ERR_STATE, "training needs online, target, grad, sq_avg and stats bound (mq_bind)");
+  int rc = check_batch(h, batch);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const Dims d = make_dims(h, batch);
+  const Rep rp = make_rep(batch);
+  const Lay L = make_lay(h);
+  Work w = h->w;
+  int32_t* curmax = h->curmax_user ? h->curmax_user : h->curmax_ws;
+  const int64_t RT = (int64_t)d.Tp * d.R;
+  PhaseTimer pt{h, s};
+  const mq_config& c = h->cfg;
+
+  pt.begin(PH_FC1);
+  {
+    Fc1Prob p{d, rp, h->on, h->tg, h->off[MQ_P_FC1_W], h->off[MQ_P_FC1_B], w.X1, RT};
+    MQ_HIP(launch_gemm(p, (int)RT, mq::H, 2, s));
+  }
+  pt.begin(PH_GI);
+  {
+    GiProb p{w.X1, h->on, h->tg, h->off[MQ_P_RNN_W_IH], h->off[MQ_P_RNN_B_IH], w.GI, RT};
+    MQ_HIP(launch_gemm(p, (int)RT, mq::G3, 2, s));
+  }
+  pt.begin(PH_GRUF);
+  {
+    const int rw = pick_rw(d.R, 512);
+    hipError_t e = rw == 1 ? launch_gru_fwd<1>(d, h, L, w, s)
+                 : rw == 2 ? launch_gru_fwd<2>(d, h, L, w, s)
+                 : rw == 4 ? launch_gru_fwd<4>(d, h, L, w, s)
+                           : launch_gru_fwd<8>(d, h, L, w, s);
+    MQ_HIP(e);
+  }
+  if (c.mixer == MQ_MIXER_QMIX) {
+    pt.begin(PH_HYP);
+    HypProb p{d, rp, L, h->on, h->tg, w.HYP};
+    MQ_HIP(launch_gemm(p, d.M, d.NH, 2, s));
+  }
+  pt.begin(PH_MIX);
+  h->nblk_mix = (d.M + 3) / 4;
+  hipLaunchKernelGGL(mix_kernel, dim3(h->nblk_mix), dim3(256), 0, s, d, rp, (const float*)h->on,
+                     (const float*)h->tg, L, w, curmax);
+  MQ_HIP(hipGetLastError());
+  pt.begin(PH_GRUB);
+  {
+    // RW = 8 would spill the 144 live accumulator/weight registers per lane; cap at 4
+    const int rw = std::min(4, pick_rw(d.R, 256));
+    hipError_t e = rw == 1 ? launch_gru_bwd<1>(d, rp, h, L, w, s, &h->nblk_bwd)
+                 : rw == 2 ? launch_gru_bwd<2>(d, rp, h, L, w, s, &h->nblk_bwd)
+                           : launch_gru_bwd<4>(d, rp, h, L, w, s, &h->nblk_bwd);
+    MQ_HIP(e);
+  }
+  pt.begin(PH_DX1);
+  {
+    Dx1Prob p{w.dGI, h->on + h->off[MQ_P_RNN_W_IH], w.X1, w.dP1, RT};
+    MQ_HIP(launch_gemm(p, (int)RT, mq::H, 1, s));
+  }
+  pt.begin(PH_DW1);
+  {
+    const int tiles = (d.I + GBN - 1) / GBN;
+    int ns = (int)std::min<int64_t>(kNsplitMax, std::max<int64_t>(1, RT / 256));
+    ns = std::max(1, std::min(ns, (512 + tiles - 1) / tiles));
+    // keep every split non-empty under krange_split's GBK rounding
+    int64_t chunk = ((RT + ns - 1) / ns + GBK - 1) / GBK * GBK;
+    ns = (int)((RT + chunk - 1) / chunk);
+    h->nsplit_fc1 = ns;
+    Dw1Prob p{d, rp, w.dP1, w.slab_fc1, RT, ns};
+    MQ_HIP(launch_gemm(p, mq::H, d.I, ns, s));
+  }
+  if (c.mixer == MQ_MIXER_QMIX) {
+    pt.begin(PH_DWH);
+    const int tiles = ((d.NH + GBM - 1) / GBM) * ((d.S + GBN - 1) / GBN);
+    int ns = std::max(1, std::min(kNsplitMax, std::min((512 + tiles - 1) / tiles, d.M / 64)));
+    int64_t chunk = ((d.M + ns - 1) / ns + GBK - 1) / GBK * GBK;
+    ns = (int)((d.M + chunk - 1) / chunk);
+    h->nsplit_mix = ns;
+    DwhProb p{d, rp, L, w.dHYP, w.slab_mix, h->len_mix, ns};
+    MQ_HIP(launch_gemm(p, d.NH, d.S, ns, s));
+  }
+  pt.begin(PH_RED);
+  if ((rc = reduce_into(w.slab_fc1, h->nsplit_fc1, (int64_t)mq::H * d.I + mq::H, h->grad + h->off[MQ_P_FC1_W], s)))
+    return rc;
+  if ((rc = reduce_into(w.slab_rnn, h->nblk_bwd, h->len_rnn, h->grad + h->off[MQ_P_RNN_W_IH], s))) return rc;
+  if (c.mixer == MQ_MIXER_QMIX) {
+    if ((rc = reduce_into(w.slab_mix, h->nsplit_mix, h->len_mix, h->grad + h->off[MQ_P_HW1_W], s))) return rc;
+    if ((rc = reduce_into(w.slab_v2, h->nblk_mix, d.E + 1, h->grad + h->off[MQ_P_V2_W], s))) return rc;
+  }
+  if ((rc = reduce_into(w.loss_part, h->nblk_mix, MQ_NSUMS, h->grad + h->P, s))) return rc;
+  pt.end();
+  h->last = d;
+  h->have_fb = true;
+  return MQ_OK;
+}
+
+int mq_apply(mq_handle* h, void* stream) {
+  if (!h || !h->on) return set_err(MQ_ERR_STATE, "mq_apply before mq_bind");
+  if (!h->have_fb) return set_err(MQ_ERR_STATE, "mq_apply before mq_forward_backward");
+  hipStream_t s = (hipStream_t)stream;
+  PhaseTimer pt{h, s};
+  pt.begin(PH_NORM);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(kNormBlocks), dim3(256), 0, s, (const float*)h->grad, h->P, h->w.norm_part);
+  MQ_HIP(hipGetLastError());
+  pt.begin(PH_APPLY);
+  OptHP hp{h->cfg.lr, h->cfg.optim_alpha, h->cfg.optim_eps, h->cfg.grad_norm_clip, h->cfg.n_agents};
+  int blocks = (int)std::min<int64_t>((h->P + 255) / 256, 1024);
+  hipLaunchKernelGGL(apply_kernel, dim3(blocks), dim3(256), 0, s, h->on, h->grad, h->sq, h->P,
+                     (const float*)h->w.norm_part, kNormBlocks, hp, h->stats);
+  MQ_HIP(hipGetLastError());
+  pt.end();
+  return MQ_OK;
+}
+
+int mq_train_step(mq_handle* h, const mq_replay* batch, void* stream) {
+  int rc = mq_forward_backward(h, batch, stream);
+  if (rc) return rc;
+  return mq_apply(h, stream);
+}
+
+int mq_update_targets(mq_handle* h, void* stream) {
+  if (!h || !h->on || !h->tg) return set_err(MQ_ERR_STATE, "mq_update_targets needs online and target bound");
+  MQ_HIP(hipMemcpyAsync(h->tg, h->on, h->P * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return MQ_OK;
+}
+
+int mq_copy_intermediate(mq_handle* h, int which, float* dst, int64_t* count, void* stream) {
+  if (!h || !h->have_fb) return set_err(MQ_ERR_STATE, "no forward/backward has run");
+  const Dims& d = h->last;
+  const int64_t RT = (int64_t)d.Tp * d.R;
+  const float* src;
+  int64_t cnt;
+  switch (which) {
+    case 0: src = h->w.Q; cnt = RT * d.A; break;
+    case 1: src = h->w.Q + RT * d.A; cnt = RT * d.A; break;
+    case 2: src = h->w.dch; cnt = (int64_t)d.T * d.R; break;
+    default: return set_err(MQ_ERR_ARG, "unknown intermediate id");
+  }
+  if (count) *count = cnt;
+  if (dst) MQ_HIP(hipMemcpyAsync(dst, src, cnt * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return MQ_OK;
+}
+
+int mq_mac_forward(mq_handle* h, const mq_replay* batch, int32_t t, const float* h_in, float* h_out, float* q_out,
+                   int32_t which, void* stream) {
+  if (!h || !h->on) return set_err(MQ_ERR_STATE, "mq_mac_forward before mq_bind");
+  if (which && !h->tg) return set_err(MQ_ERR_STATE, "target parameters not bound");
+  if (!batch || !batch->obs || !batch->actions || !batch->filled || !h_in || !h_out || !q_out)
+    return set_err(MQ_ERR_ARG, "NULL pointer in mq_mac_forward");
+  if (t < 0 || t >= batch->t_stride) return set_err(MQ_ERR_ARG, "t outside the stored episode");
+  if (batch->batch_size < 1) return set_err(MQ_ERR_ARG, "empty batch");
+  mq_replay b = *batch;
+  b.t_len = std::max(2, std::min(b.t_stride, 2));
+  const Dims d = make_dims(h, &b);
+  const Rep rp = make_rep(batch);
+  const Lay L = make_lay(h);
+  const size_t smem = (size_t)(((d.I + 3) & ~3) + mq::H * 3 + mq::G3 * 2) * sizeof(float);
+  hipLaunchKernelGGL(mac_step_kernel, dim3(d.R), dim3(256), smem, (hipStream_t)stream, d, rp,
+                     (const float*)(which ? h->tg : h->on), L, (int)t, (const float*)nullptr, h_in, h_out, q_out);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+int mq_agent_forward(mq_handle* h, const float* inputs, int32_t rows, const float* h_in, float* h_out, float* q_out,
+                     int32_t which, void* stream) {
+  if (!h || !h->on) return set_err(MQ_ERR_STATE, "mq_agent_forward before mq_bind");
+  if (which && !h->tg) return set_err(MQ_ERR_STATE, "target parameters not bound");
+  if (!inputs || !h_in || !h_out || !q_out || rows < 0) return set_err(MQ_ERR_ARG, "bad mq_agent_forward args");
+  if (rows == 0) return MQ_OK;
+  mq_replay b;
+  std::memset(&b, 0, sizeof(b));
+  b.batch_size = 1; b.t_len = 2; b.t_stride = 2;
+  Dims d = make_dims(h, &b);
+  d.n = 1;   // rows are independent here: block -> row, agent id unused
+  const Rep rp = make_rep(&b);
+  const Lay L = make_lay(h);
+  const size_t smem = (size_t)(((d.I + 3) & ~3) + mq::H * 3 + mq::G3 * 2) * sizeof(float);
+  hipLaunchKernelGGL(mac_step_kernel, dim3(rows), dim3(256), smem, (hipStream_t)stream, d, rp,
+                     (const float*)(which ? h->tg : h->on), L, 0, inputs, h_in, h_out, q_out);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+int mq_greedy_actions(const float* q, const int32_t* avail, int64_t* out, int32_t rows, int32_t n_actions,
+                      void* stream) {
+  if (!q || !avail || !out || rows < 0 || n_actions < 1) return set_err(MQ_ERR_ARG, "bad mq_greedy_actions args");
+  if (rows == 0) return MQ_OK;
+  hipLaunchKernelGGL(greedy_kernel, dim3((rows + 255) / 256), dim3(256), 0, (hipStream_t)stream, q, avail, out,
+                     (int)rows, (int)n_actions);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+int mq_set_timing(mq_handle* h, int32_t on) {
+  if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
+  if (on && !h->ev_made) {
+    for (int p = 0; p < PH_N; ++p) {
+      MQ_HIP(hipEventCreate(&h->ev0[p]));
+      MQ_HIP(hipEventCreate(&h->ev1[p]));
+    }
+    h->ev_made = true;
+  }
+  h->timing = on != 0;
+  for (int p = 0; p < PH_N; ++p) h->ev_used[p] = false;
+  return MQ_OK;
+}
+
+int mq_phase_times(mq_handle* h, float* ms, int32_t cap, int32_t* n) {
+  if (!h || !ms) return set_err(MQ_ERR_ARG, "NULL argument");
+  if (n) *n = PH_N;
+  for (int p = 0; p < PH_N && p < cap; ++p) {
+    ms[p] = 0.0f;
+    if (h->ev_made && h->ev_used[p]) {
+      MQ_HIP(hipEventSynchronize(h->ev1[p]));
+      MQ_HIP(hipEventElapsedTime(&ms[p], h->ev0[p], h->ev1[p]));
+    }
+  }
+  return MQ_OK;
+}
+
+}  // extern "C"

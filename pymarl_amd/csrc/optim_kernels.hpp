@@ -1,0 +1,160 @@
+// Gradient slab reduction, clip_grad_norm_ and RMSprop over the flat parameter vector (q_learner.py:100-103),
+// plus the single-step agent forward and greedy selection used on the rollout side
+// (basic_controller.py:40-75, action_selectors.py:44-62).
+#pragma once
+#include "learner_types.hpp"
+
+namespace mq {
+
+// dst[i] = sum_z slab[z*len + i], z in order (bitwise reproducible).
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restrict__ slab, int nslab, int64_t len,
+                                                           float* __restrict__ dst) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < len; i += (int64_t)gridDim.x * 256) {
+    float s = 0.0f;
+    for (int z = 0; z < nslab; ++z) s += slab[(int64_t)z * len + i];
+    dst[i] = s;
+  }
+}
+
+// Per-block partial sum of squares of the (unnormalised) gradient.
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, int64_t n, float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.0f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) s = fmaf(g[i], g[i], s);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+struct OptHP {
+  float lr, alpha, eps, clip;
+  int n_agents;
+};
+
+// Normalise by sum(mask), clip by the global norm (torch clip_grad_norm_: coef = clip / (norm + 1e-6),
+// clamped to 1), RMSprop (torch: v = a v + (1-a) g^2; p += -lr * g / (sqrt(v) + eps)). Every block re-derives
+// the norm from the same partials in the same order, so all blocks agree bitwise.
+__global__ __launch_bounds__(256) void apply_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ sq,
+                                                    int64_t n, const float* __restrict__ part, int npart,
+                                                    OptHP hp, float* __restrict__ stats) {
+  __shared__ float sh[2];
+  if (threadIdx.x < 64) {
+    float s = 0.0f;
+    for (int i = threadIdx.x; i < npart; i += 64) s += part[i];
+    s = wave_sum(s);
+    if (threadIdx.x == 0) sh[0] = s;
+  }
+  __syncthreads();
+  const float* sums = g + n;   // MQ_NSUMS tail
+  const float msum = sums[1];
+  const float inv = 1.0f / msum;
+  const float norm = sqrtf(sh[0]) * inv;
+  const float coef = fminf(hp.clip / (norm + 1e-6f), 1.0f);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float gi = (g[i] * inv) * coef;
+    g[i] = gi;
+    const float v = sq[i] * hp.alpha + (1.0f - hp.alpha) * (gi * gi);
+    sq[i] = v;
+    p[i] = p[i] + (-hp.lr) * (gi / (sqrtf(v) + hp.eps));
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    stats[0] = sums[0] / msum;                         // loss
+    stats[1] = norm;                                   // grad_norm
+    stats[2] = sums[2] / msum;                         // td_error_abs
+    stats[3] = sums[3] / (msum * (float)hp.n_agents);  // q_taken_mean (q_learner.py:114 divisor)
+    stats[4] = sums[4] / (msum * (float)hp.n_agents);  // target_mean
+    stats[5] = msum;
+    stats[6] = coef;
+    stats[7] = 0.0f;
+  }
+}
+
+// One BasicMAC.forward step for every (episode, agent) row: inputs [obs_t | onehot(a_{t-1}) | onehot(agent)],
+// fc1 -> relu -> GRUCell -> fc2. One 256-thread workgroup per row (rollout batches are small).
+// xin_dense != NULL: the inputs are given ([rows][I], RNNAgent.forward); otherwise they are built from the replay.
+__global__ __launch_bounds__(256) void mac_step_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L, int t,
+                                                       const float* __restrict__ xin_dense,
+                                                       const float* __restrict__ h_in, float* __restrict__ h_out,
+                                                       float* __restrict__ q_out) {
+  extern __shared__ float sm[];   // xin [I] | x1 [H] | h [H] | gi [3H] | gh [3H] | h1 [H]
+  float* xin = sm;
+  float* x1 = xin + ((d.I + 3) & ~3);
+  float* hh = x1 + H;
+  float* gi = hh + H;
+  float* gh = gi + G3;
+  float* h1 = gh + G3;
+  const int row = blockIdx.x, b = row / d.n, ag = row - b * d.n, tid = threadIdx.x;
+  const int64_t slot = xin_dense ? 0 : rp.ep(b) * d.t_stride + t;
+  for (int f = tid; f < d.I; f += 256) {
+    float v;
+    if (xin_dense) {
+      v = xin_dense[(int64_t)row * d.I + f];
+    } else if (f < d.O) {
+      v = rp.obs[(slot * d.n + ag) * d.O + f];
+    } else {
+      int g = f - d.O;
+      v = 0.0f;
+      bool done = false;
+      if (d.last_action) {
+        if (g < d.A) {
+          if (t > 0 && rp.filled[slot - 1]) v = (int)rp.actions[(slot - 1) * d.n + ag] == g ? 1.0f : 0.0f;
+          done = true;
+        }
+        g -= d.A;
+      }
+      if (!done) v = (d.agent_id && g == ag) ? 1.0f : 0.0f;
+    }
+    xin[f] = v;
+  }
+  if (tid < H) hh[tid] = h_in[(int64_t)row * H + tid];
+  __syncthreads();
+  if (tid < H) {
+    const float* w = P + L.o[MQ_P_FC1_W] + (int64_t)tid * d.I;
+    float s = 0.0f;
+    for (int k = 0; k < d.I; ++k) s = fmaf(w[k], xin[k], s);
+    x1[tid] = fmaxf(s + P[L.o[MQ_P_FC1_B] + tid], 0.0f);
+  }
+  __syncthreads();
+  if (tid < G3) {
+    const float* wi = P + L.o[MQ_P_RNN_W_IH] + tid * H;
+    const float* wh = P + L.o[MQ_P_RNN_W_HH] + tid * H;
+    float si = 0.0f, shh = 0.0f;
+    for (int k = 0; k < H; ++k) { si = fmaf(wi[k], x1[k], si); shh = fmaf(wh[k], hh[k], shh); }
+    gi[tid] = si + P[L.o[MQ_P_RNN_B_IH] + tid];
+    gh[tid] = shh + P[L.o[MQ_P_RNN_B_HH] + tid];
+  }
+  __syncthreads();
+  if (tid < H) {
+    const float r = sigmoidf_(gh[tid] + gi[tid]);
+    const float zg = sigmoidf_(gh[H + tid] + gi[H + tid]);
+    const float ng = tanhf_(gi[2 * H + tid] + gh[2 * H + tid] * r);
+    const float v = (hh[tid] - ng) * zg + ng;
+    h1[tid] = v;
+  }
+  __syncthreads();
+  if (tid < H) h_out[(int64_t)row * H + tid] = h1[tid];
+  if (tid < d.A) {
+    const float* w = P + L.o[MQ_P_FC2_W] + tid * H;
+    float s = 0.0f;
+    for (int k = 0; k < H; ++k) s = fmaf(w[k], h1[k], s);
+    q_out[(int64_t)row * d.A + tid] = s + P[L.o[MQ_P_FC2_B] + tid];
+  }
+}
+
+// Masked greedy argmax (unavailable = -inf, first max index), one lane per row.
+__global__ __launch_bounds__(256) void greedy_kernel(const float* __restrict__ q, const int32_t* __restrict__ avail,
+                                                     int64_t* __restrict__ out, int rows, int A) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= rows) return;
+  float best = 0.0f;
+  int arg = 0;
+  bool any = false;
+  for (int a = 0; a < A; ++a) {
+    const float v = avail[(int64_t)row * A + a] ? q[(int64_t)row * A + a] : -INFINITY;
+    if (!any || v > best) { best = v; arg = a; any = true; }
+  }
+  out[row] = arg;
+}
+
+}  // namespace mq
