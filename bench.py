@@ -1,0 +1,264 @@
+"""Learner throughput bench: QLearner.train on synthetic replay, MI355X, 1..8 GPUs (one process per GPU).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4] [--no-cpu-baseline]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+
+Metric (BASELINE.json): learner samples/s = B*T*n_agents per train() / wall seconds, whole job (all ranks).
+Default workload = BASELINE configs[1]: QMIX synthetic replay n_agents=8, T=120, obs=80, state=168, batch=32 per
+GPU (weak scaling: every rank trains its own 32-episode shard of one global sample and the ranks all-reduce the
+gradient once per step over RCCL). The replay (5000 episodes, SURVEY.md §8d recipe) lives in HBM; a step is the
+full train(): id sampling on the host, fused gather, both unrolls, double-Q, mixer, loss, BPTT, clip, RMSprop,
+the episode-counted target update — nothing skipped.
+
+The JSON line also carries:
+* roofline: the dominant kernel (longest mean duration over the timed steps, HIP events on the learner's stream)
+  priced by its ALGORITHMIC fp32 flops per launch (DESIGN.md "Roofline") against the gfx950 fp32 peak;
+  `traffic` = PMC-measured HBM bytes per launch of that kernel, read from profiles/ if a pmc summary for this
+  config is committed there (null otherwise).
+* cpu_baseline: the numpy oracle's train() (oracle/qlearner_np.py, a restatement of the reference's QLearner.train
+  pinned to golden vectors of the reference itself) timed on this host, rank 0 at N=1 only, on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import sys
+import time
+from types import SimpleNamespace as SN
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "learner samples/sec (B×T×n_agents), synthetic replay, 1/2/4/8 MI355X"
+FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: fp32 vector = fp32 matrix peak
+HBM_PEAK_GBS = 8000.0
+
+CONFIGS = {
+    # name: (mixer, n, A, O, S, T, B, description)
+    "cfg2": ("qmix", 8, 14, 80, 168, 120, 32, "QMIX synthetic replay n_agents=8 T=120 obs=80 state=168 batch=32"),
+    "cfg3": ("vdn", 27, 36, 285, 1170, 180, 128, "VDN synthetic 27m_vs_30m shape n_agents=27 T=180 batch=128"),
+    "cfg4": ("qmix", 5, 11, 80, 120, 120, 64, "QMIX 2s3z shape, 64 episodes per GPU (512 over 8 GPUs)"),
+}
+
+
+def algorithmic_flops(phase, n, A, O, S, T, B, E=32, H=64, mixer="qmix"):
+    """fp32 flops one launch of `phase` must do (matmul terms, 2 flop per MAC; elementwise ignored)."""
+    Tp = T + 1
+    R = B * n
+    RT = Tp * R
+    I = O + A + n
+    NH = E * (n + 3)
+    M = T * B
+    f = {
+        "fc1": 2 * 2 * RT * H * O,                          # both nets, obs part (one-hot columns are gathers)
+        "gi": 2 * 2 * RT * 3 * H * H,                       # both nets
+        "gru_fwd": 2 * 2 * RT * (3 * H * H + H * A),        # W_hh mat-vec + fc2, both nets
+        "hyper": 2 * 2 * M * NH * S if mixer == "qmix" else 0,
+        "gru_bwd": 2 * RT * (3 * H * H) * 3,                # W_hh^T mat-vec + dW_hh + dW_ih accumulations
+        "dx1": 2 * RT * 3 * H * H,
+        "dw1": 2 * RT * H * I,
+        "dwh": 2 * M * NH * S if mixer == "qmix" else 0,
+    }
+    return f.get(phase)
+
+
+def build_workload(cfg_name, device, n_episodes=5000, unique=512, seed=0):
+    import torch as th
+    from pymarl_amd.components.episode_buffer import ReplayBuffer
+    from pymarl_amd.components.transforms import OneHot
+    from pymarl_amd.controllers import REGISTRY as mac_REGISTRY
+    from pymarl_amd.learners import REGISTRY as le_REGISTRY
+    from pymarl_amd.utils.logging import Logger
+    from pymarl_amd.utils.synthetic import make_replay
+
+    mixer, n, A, O, S, T, B, _ = CONFIGS[cfg_name]
+    args = SN(n_agents=n, n_actions=A, state_shape=S, obs_shape=O, rnn_hidden_dim=64, mixing_embed_dim=32,
+              mixer=mixer, lr=5e-4, optim_alpha=0.99, optim_eps=1e-5, grad_norm_clip=10.0, gamma=0.99,
+              double_q=True, target_update_interval=200, learner_log_interval=10 ** 12, obs_last_action=True,
+              obs_agent_id=True, agent="rnn", mac="basic_mac", agent_output_type="q",
+              action_selector="epsilon_greedy", epsilon_start=1.0, epsilon_finish=0.05, epsilon_anneal_time=50000,
+              batch_size=B, learner="q_learner", learner_dp=True, device=str(device), use_cuda=True)
+    scheme = {
+        "state": {"vshape": S},
+        "obs": {"vshape": O, "group": "agents"},
+        "actions": {"vshape": (1,), "group": "agents", "dtype": th.long},
+        "avail_actions": {"vshape": (A,), "group": "agents", "dtype": th.int},
+        "reward": {"vshape": (1,)},
+        "terminated": {"vshape": (1,), "dtype": th.uint8},
+    }
+    groups = {"agents": n}
+    buf = ReplayBuffer(scheme, groups, n_episodes, T + 1, preprocess={"actions": ("actions_onehot", [OneHot(A)])},
+                       device=device)
+    data = make_replay(unique, T, n, A, O, S, seed=seed)
+    for start in range(0, n_episodes, unique):   # tile the unique episodes across the HBM-resident buffer
+        m = min(unique, n_episodes - start)
+        for k, v in data.items():
+            buf.data.transition_data[k][start:start + m] = th.as_tensor(v[:m], device=device)
+    buf.episode_lengths[:] = buf.data.transition_data["filled"].sum(1).reshape(-1).cpu().numpy()
+    buf.episodes_in_buffer = n_episodes
+    mac = mac_REGISTRY["basic_mac"](buf.scheme, groups, args)
+    learner = le_REGISTRY["q_learner"](mac, buf.scheme, Logger(logging.getLogger("bench")), args)
+    learner.cuda()
+    return args, buf, learner, data
+
+
+def cpu_baseline(cfg_name, data, budget_s=12.0):
+    """Time the numpy oracle's train() on this host's cores (bounded sample)."""
+    from oracle.qlearner_np import OracleQLearner
+    from pymarl_amd.utils.synthetic import agent_param_shapes, init_params, qmix_param_shapes
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    mixer, n, A, O, S, T, B, _ = CONFIGS[cfg_name]
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    cfg = dict(n_agents=n, n_actions=A, mixer=mixer, gamma=0.99, lr=5e-4, optim_alpha=0.99, optim_eps=1e-5,
+               grad_norm_clip=10.0, double_q=True, target_update_interval=200, learner_log_interval=0)
+    ap = init_params(agent_param_shapes(O + A + n, 64, A), 1)
+    mp = init_params(qmix_param_shapes(S, n, 32), 101) if mixer == "qmix" else {}
+    o = OracleQLearner(ap, mp, cfg)
+    rng = np.random.RandomState(7)
+    ctx = threadpool_limits(limits=cores) if threadpool_limits else None
+    times = []
+    t_start = time.perf_counter()
+    try:
+        while True:
+            ids = rng.choice(len(data["obs"]), B, replace=False)
+            batch = {k: v[ids] for k, v in data.items()}
+            t0 = time.perf_counter()
+            o.train(batch, 0, len(times))
+            times.append(time.perf_counter() - t0)
+            if time.perf_counter() - t_start > budget_s and len(times) >= 2:
+                break
+    finally:
+        if ctx is not None:
+            ctx.unregister() if hasattr(ctx, "unregister") else None
+    s = float(np.median(times))
+    return {"value": B * T * n / s, "unit": "samples/s", "cores": cores, "kind": "port",
+            "sample": f"{len(times)} numpy-oracle train() steps of {cfg_name} (B={B}, T={T}, n={n}), "
+                      f"median {s * 1e3:.1f} ms/step, {cores} BLAS threads"}
+
+
+def pmc_traffic(cfg_name, phase):
+    """HBM bytes per launch of `phase` from a committed PMC summary (profiles/*pmc*.json), else None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            v = d.get(cfg_name, {}).get(phase, {}).get("hbm_bytes_per_launch")
+            if v:
+                return float(v)
+        except Exception:
+            continue
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--phases", action="store_true", help="print every phase's mean ms to stderr")
+    a = ap.parse_args()
+
+    import torch as th
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        th.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=th.device("cuda", local_rank))
+    device = th.device("cuda", local_rank)
+    th.cuda.set_device(device)
+
+    args, buf, learner, data = build_workload(a.config, device)
+    mixer, n, A, O, S, T, B, desc = CONFIGS[a.config]
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    np.random.seed(2)
+    episode = 0
+
+    def step(k):
+        nonlocal episode
+        gb = buf.sample(B * world)
+        batch = gb.shard(rank, world) if world > 1 else gb
+        batch = batch[:, :batch.max_t_filled()]
+        learner.train(batch, t_env=1000 * k, episode_num=episode)
+        episode += 8   # batch_size_run episodes per outer-loop iteration (run.py:247, qmix_smac.yaml:10)
+
+    for k in range(max(1, a.warmup)):
+        step(k)
+    th.cuda.synchronize()
+    # phase survey (untimed): which kernel dominates
+    names = learner.phase_names()
+    learner.set_timing(slots=4)
+    for k in range(4):
+        step(k)
+    th.cuda.synchronize()
+    survey = learner.phase_times()
+    dominant = max(survey, key=survey.get)
+    # timed region: events around the dominant kernel only
+    learner.set_timing(slots=min(a.steps, 4096), phases=[dominant])
+    barrier()
+    th.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        step(k)
+    th.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    dom_ms = learner.phase_times()[dominant]
+    learner.set_timing(slots=0)
+    if world > 1:
+        t = th.tensor([dt], dtype=th.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    samples = B * T * n * world * a.steps
+    value = samples / dt
+    if rank == 0:
+        if a.phases:
+            print(json.dumps({"phase_ms": survey}), file=sys.stderr)
+        fl = algorithmic_flops(dominant, n, A, O, S, T, B, mixer=mixer)
+        achieved = (fl / (dom_ms * 1e-3) / 1e12) if (fl and dom_ms > 0) else None
+        traffic = pmc_traffic(a.config, dominant)
+        roof = {"bound": "mfma", "kernel": dominant, "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": (achieved / FP32_PEAK_TFLOPS) if achieved else None,
+                "traffic": traffic, "launch_ms": dom_ms, "flops_per_launch": fl}
+        cpu = None
+        if world == 1 and not a.no_cpu_baseline:
+            cpu = cpu_baseline(a.config, data)
+        bytes_per_sample = (O * 4 + (S * 4) / n + 8 + A * 4 + (4 + 1 + 8) / n)   # read-once replay bytes
+        line = {
+            "metric": METRIC, "value": value, "unit": "samples/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (SURVEY.md §8d replay recipe, random-init weights)",
+            "config": {"workload": desc, "mixer": mixer, "n_agents": n, "n_actions": A, "obs_dim": O,
+                       "state_dim": S, "episode_limit": T, "batch_per_gpu": B, "global_batch": B * world,
+                       "replay_episodes": buf.buffer_size, "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "hbm_roofline_whole_step": {"achieved_GBs": value * bytes_per_sample / 1e9, "peak_GBs": HBM_PEAK_GBS,
+                                        "frac": value * bytes_per_sample / 1e9 / HBM_PEAK_GBS},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -104,9 +104,10 @@ int mq_agent_forward(mq_handle* h, const float* inputs, int32_t rows, const floa
 int mq_greedy_actions(const float* q, const int32_t* avail, int64_t* out, int32_t rows, int32_t n_actions,
                       void* stream);
 
-/* Optional per-kernel HIP-event timing of the train step (bench / profiling). */
-int mq_set_timing(mq_handle* h, int32_t on);
-/* After a synchronised step: ms per phase; names of the phases as a ';'-separated list. */
+/* Optional per-kernel HIP-event timing of train steps (bench / profiling): events bracket every phase whose bit
+ * is set in phase_mask (bit i = phase i of mq_phase_names), in a ring of `slots` steps; slots = 0 turns it off. */
+int mq_set_timing(mq_handle* h, int32_t slots, uint32_t phase_mask);
+/* Mean ms per phase over the recorded steps (synchronises on the events); *n = number of phases. */
 int mq_phase_times(mq_handle* h, float* ms, int32_t cap, int32_t* n);
 const char* mq_phase_names(void);
 

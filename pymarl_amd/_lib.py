@@ -83,7 +83,7 @@ def load(required=True):
         "mq_mac_forward": ([vp, ctypes.POINTER(MQReplay), i32, vp, vp, vp, i32, vp], ctypes.c_int),
         "mq_agent_forward": ([vp, vp, i32, vp, vp, vp, i32, vp], ctypes.c_int),
         "mq_greedy_actions": ([vp, vp, vp, i32, i32, vp], ctypes.c_int),
-        "mq_set_timing": ([vp, i32], ctypes.c_int),
+        "mq_set_timing": ([vp, i32, ctypes.c_uint32], ctypes.c_int),
         "mq_phase_times": ([vp, ctypes.POINTER(ctypes.c_float), i32, ctypes.POINTER(i32)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():

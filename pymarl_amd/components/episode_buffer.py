@@ -89,7 +89,7 @@ class EpisodeBatch:
                 if mark_filled:
                     target["filled"][slices] = 1
                     mark_filled = False
-                _slices = slices
+                _slices = tuple(slices)
             elif k in self.data.episode_data:
                 target = self.data.episode_data
                 _slices = slices[0]
@@ -189,7 +189,12 @@ class SampledBatch(EpisodeBatch):
     def __init__(self, source, ep_ids, t_len=None):
         self.source = source
         self.ep_ids_np = np.asarray(ep_ids, dtype=np.int64)
-        self.ep_ids = th.as_tensor(self.ep_ids_np, device=source.device)
+        host = th.from_numpy(self.ep_ids_np)
+        if th.device(source.device).type == "cuda":
+            # pinned + async: the id upload is stream-ordered and never stalls the host on earlier kernels
+            self.ep_ids = host.pin_memory().to(source.device, non_blocking=True)
+        else:
+            self.ep_ids = host.to(source.device)
         self.t_len = source.max_seq_length if t_len is None else int(t_len)
         super().__init__(source.scheme, source.groups, len(self.ep_ids_np), self.t_len,
                          data=SN(transition_data=_LazyGather(self, True), episode_data=_LazyGather(self, False)),
@@ -199,11 +204,20 @@ class SampledBatch(EpisodeBatch):
         if isinstance(item, tuple) and len(item) == 2 and isinstance(item[0], slice) and item[0] == slice(None) \
                 and isinstance(item[1], slice) and item[1].start in (None, 0) and item[1].step in (None, 1):
             stop = self.t_len if item[1].stop is None else min(int(item[1].stop), self.t_len)
-            return SampledBatch(self.source, self.ep_ids_np, stop)
+            return SampledBatch._view(self, stop)
         if isinstance(item, str):
             return self.data.episode_data[item] if item in self.source.data.episode_data \
                 else self.data.transition_data[item]
         return self.materialize()[item]
+
+    @classmethod
+    def _view(cls, other, t_len):
+        new = cls.__new__(cls)
+        new.source, new.ep_ids_np, new.ep_ids, new.t_len = other.source, other.ep_ids_np, other.ep_ids, int(t_len)
+        EpisodeBatch.__init__(new, other.source.scheme, other.source.groups, len(other.ep_ids_np), new.t_len,
+                              data=SN(transition_data=_LazyGather(new, True), episode_data=_LazyGather(new, False)),
+                              preprocess=None, device=other.source.device)
+        return new
 
     def materialize(self):
         """The reference's EpisodeBatch for these ids (episode_buffer.py:205-217 gather + time truncation)."""
@@ -220,8 +234,8 @@ class SampledBatch(EpisodeBatch):
 
     def shard(self, rank, world):
         """Contiguous slice [rank*B/world, (rank+1)*B/world) of the episodes (data-parallel learner)."""
-        B = len(self.ep_ids_np)
-        lo, hi = rank * B // world, (rank + 1) * B // world
+        from ..learners.dp import shard_bounds
+        lo, hi = shard_bounds(len(self.ep_ids_np), rank, world)
         return SampledBatch(self.source, self.ep_ids_np[lo:hi], self.t_len)
 
     def to(self, device):

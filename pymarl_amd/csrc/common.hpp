@@ -47,6 +47,17 @@ MQ_DEV float quad_sum(float v) {
   return v + quad_xor2(v);
 }
 
+// Workgroup barrier that orders LDS only. __syncthreads() is a workgroup-scope release, which on gfx950 also
+// drains every outstanding global load/store (s_waitcnt vmcnt(0)) at each barrier: in the persistent T loops that
+// serialised every step behind its own output stores and the next step's prefetch. Nothing in those loops
+// communicates through global memory inside the workgroup, so an LDS-only barrier is sufficient.
+// s_waitcnt vmcnt(0) as a real instruction (visible to the compiler's wait-count pass). Issued once after a
+// kernel's prologue loads so the loop header does not inherit them: otherwise the loop's first use of a
+// prologue register is guarded by a vmcnt(N) that, in steady state, also waits for the previous step's stores.
+MQ_DEV void drain_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+MQ_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 MQ_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

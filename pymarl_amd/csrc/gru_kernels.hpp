@@ -27,7 +27,9 @@ MQ_DEV float pick_row(const float (&v)[RW], int ii, int q) {
 
 // ------------------------------------------------------------------------------------------------ forward
 // grid = (ceil(R / RW), 2 nets). Writes Q for both nets; Hs and Gates for the online net only.
-template <int RW>
+// VAR: ablation bits for scripts/rec_micro.hip only (production = 0): 1 skip Hs/Gates stores, 2 skip fc2,
+// 4 skip the GI prefetch (load at use).
+template <int RW, int VAR = 0>
 __global__ __launch_bounds__(256) void gru_fwd_kernel(Dims d, const float* __restrict__ P0,
                                                       const float* __restrict__ P1, Lay L, Work w) {
   constexpr int RL = (RW + 3) / 4;   // rows per lane in the gate phase
@@ -77,13 +79,14 @@ __global__ __launch_bounds__(256) void gru_fwd_kernel(Dims d, const float* __res
     }
   };
   load_gi(0);
-  __syncthreads();
+  drain_vmem();
+  lds_barrier();
 
   for (int t = 0; t < d.Tp; ++t) {
     float cr[RL], cz[RL], cn[RL];
 #pragma unroll
     for (int ii = 0; ii < RL; ++ii) { cr[ii] = gi_r[ii]; cz[ii] = gi_z[ii]; cn[ii] = gi_n[ii]; }
-    load_gi(t + 1);   // prefetch the next step's input gates under this step's mat-vec
+    if (!(VAR & 4)) load_gi(t + 1);   // prefetch the next step's input gates under this step's mat-vec
 
     float (*hb)[H] = hbuf[t & 1];
     float (*hn)[H] = hbuf[(t + 1) & 1];
@@ -119,7 +122,7 @@ __global__ __launch_bounds__(256) void gru_fwd_kernel(Dims d, const float* __res
         const float ng = tanhf_(cn[ii] + ghn * rg);
         const float h1 = (hp - ng) * zg + ng;   // ATen gru_cell: (hx - n) * z + n
         hn[i][j] = h1;
-        if (z == 0 && r < R) {
+        if (!(VAR & 1) && z == 0 && r < R) {
           const int64_t tr = (int64_t)t * R + r;
           w.Hs[tr * H + j] = h1;
           float* g = w.Gates + tr * (4 * H);
@@ -127,10 +130,11 @@ __global__ __launch_bounds__(256) void gru_fwd_kernel(Dims d, const float* __res
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
+    if (VAR & 4) load_gi(t + 1);
     // fc2 on the new hidden state: q = W2 h + b2 (rnn_agent.py:35)
 #pragma unroll
-    for (int i = 0; i < RW; ++i) {
+    for (int i = 0; i < (VAR & 2 ? 0 : RW); ++i) {
       const f32x4* hv4 = (const f32x4*)(&hn[i][16 * q]);
       float s = 0.0f, s2 = 0.0f;
 #pragma unroll
@@ -179,7 +183,8 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(Dims d, Rep rp, const floa
   float dbi0 = 0, dbi1 = 0, dbi2 = 0, dbh2 = 0;
 #pragma unroll
   for (int ii = 0; ii < RL; ++ii) { carry[ii] = 0.0f; cz[ii] = 0.0f; ht[ii] = 0.0f; }
-  __syncthreads();
+  drain_vmem();
+  lds_barrier();
 
   for (int t = d.Tp - 1; t >= 0; --t) {
     const int pb = t & 1;
@@ -238,7 +243,7 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(Dims d, Rep rp, const floa
         __builtin_amdgcn_wave_barrier();
       }
     }
-    __syncthreads();
+    lds_barrier();
     float s[RW];
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(Dims d, Rep rp, const floa
     slab[o_bi + k] = dbi0; slab[o_bi + H + k] = dbi1; slab[o_bi + 2 * H + k] = dbi2;
     slab[o_bh + k] = dbi0; slab[o_bh + H + k] = dbi1; slab[o_bh + 2 * H + k] = dbh2;
   }
-  __syncthreads();
+  lds_barrier();
   for (int i = tid; i < A * H; i += 256) slab[o_w2 + i] = dw2_s[i];
   for (int i = tid; i < A; i += 256) slab[o_b2 + i] = db2_s[i];
 }

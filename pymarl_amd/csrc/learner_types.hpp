@@ -54,6 +54,7 @@ struct Work {
   float* loss_part;  // [mix blocks][8]
   float* norm_part;  // [norm blocks]
   int32_t* curmax;   // [T*R]
+  float* red_tmp;    // two-pass slab reduction partials
 };
 
 MQ_DEV void split_tr(const Dims& d, uint32_t tr, int& t, int& r, int& b, int& ag) {

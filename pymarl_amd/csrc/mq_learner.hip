@@ -15,9 +15,11 @@
 //   norm     partial sum of squares
 //   apply    / sum(mask), clip_grad_norm_, RMSprop
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "learner_gemms.hpp"
 #include "gru_kernels.hpp"
@@ -76,11 +78,12 @@ struct mq_handle {
   bool have_fb = false;
   Dims last;
   int nsplit_fc1 = 1, nsplit_mix = 1, nblk_bwd = 1, nblk_mix = 1;
-  // timing
-  bool timing = false;
-  hipEvent_t ev0[PH_N], ev1[PH_N];
-  bool ev_used[PH_N];
-  bool ev_made = false;
+  // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
+  int slots = 0;
+  uint32_t mask = 0;
+  int64_t tstep = 0;
+  std::vector<hipEvent_t> ev0, ev1;
+  std::vector<uint8_t> ev_used;
 };
 
 namespace {
@@ -156,16 +159,17 @@ struct PhaseTimer {
   mq_handle* h;
   hipStream_t s;
   int cur = -1;
+  int idx(int p) const { return (int)(h->tstep % h->slots) * PH_N + p; }
   void begin(int p) {
-    if (!h->timing) return;
     end();
-    (void)hipEventRecord(h->ev0[p], s);
-    h->ev_used[p] = true;
+    if (h->slots <= 0 || !((h->mask >> p) & 1u)) return;
+    (void)hipEventRecord(h->ev0[idx(p)], s);
+    h->ev_used[idx(p)] = 1;
     cur = p;
   }
   void end() {
-    if (!h->timing || cur < 0) return;
-    (void)hipEventRecord(h->ev1[cur], s);
+    if (cur < 0) return;
+    (void)hipEventRecord(h->ev1[idx(cur)], s);
     cur = -1;
   }
 };
@@ -187,10 +191,18 @@ hipError_t launch_gru_bwd(const Dims& d, const Rep& rp, const mq_handle* h, cons
   return hipGetLastError();
 }
 
-int reduce_into(const float* slab, int nslab, int64_t len, float* dst, hipStream_t s) {
+int reduce_into(const float* slab, int nslab, int64_t len, float* dst, float* tmp, hipStream_t s) {
   if (len <= 0) return MQ_OK;
-  int blocks = (int)std::min<int64_t>((len + 255) / 256, 2048);
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(blocks), dim3(256), 0, s, slab, nslab, len, dst);
+  const unsigned bx = (unsigned)((len + 255) / 256);
+  if (nslab <= 2 * kRedZ) {
+    hipLaunchKernelGGL(reduce_slabs_kernel, dim3(bx, 1), dim3(256), 0, s, slab, nslab, len, nslab, dst);
+    MQ_HIP(hipGetLastError());
+    return MQ_OK;
+  }
+  const int nz = (nslab + kRedZ - 1) / kRedZ;
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(bx, nz), dim3(256), 0, s, slab, nslab, len, kRedZ, tmp);
+  MQ_HIP(hipGetLastError());
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(bx, 1), dim3(256), 0, s, (const float*)tmp, nz, len, nz, dst);
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }
@@ -232,7 +244,12 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
   const int64_t Rm = (int64_t)c.max_batch * n;
   const int64_t nmix = (Mm + 3) / 4;
   const int64_t NH = h->NH;
-  int64_t sizes[17] = {
+  const int64_t red_tmp = std::max({((Rm + kRedZ - 1) / kRedZ) * h->len_rnn,
+                                    (int64_t)((kNsplitMax + kRedZ - 1) / kRedZ) * (Hd * h->I + Hd),
+                                    (int64_t)((kNsplitMax + kRedZ - 1) / kRedZ) * h->len_mix,
+                                    ((nmix + kRedZ - 1) / kRedZ) * (h->E + 1),
+                                    ((nmix + kRedZ - 1) / kRedZ) * 8});
+  int64_t sizes[18] = {
       2 * RT * Hd,                                   // X1
       2 * RT * 3 * Hd,                               // GI
       RT * Hd,                                       // Hs
@@ -250,9 +267,10 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
       nmix * 8,                                      // loss_part
       kNormBlocks,                                   // norm_part
       Mm * n,                                        // curmax (int32)
+      red_tmp,                                       // two-pass reduction partials
   };
-  int64_t total = 0, offs[17];
-  for (int i = 0; i < 17; ++i) { offs[i] = total; total += align_up(std::max<int64_t>(sizes[i], 1)); }
+  int64_t total = 0, offs[18];
+  for (int i = 0; i < 18; ++i) { offs[i] = total; total += align_up(std::max<int64_t>(sizes[i], 1)); }
   hipError_t e = hipMalloc(&h->ws, total * sizeof(float));
   if (e != hipSuccess) {
     delete h;
@@ -267,16 +285,16 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
   w.slab_mix = base + offs[12]; w.slab_v2 = base + offs[13]; w.loss_part = base + offs[14];
   w.norm_part = base + offs[15];
   h->curmax_ws = (int32_t*)(base + offs[16]);
+  w.red_tmp = base + offs[17];
   w.curmax = h->curmax_ws;
-  for (int p = 0; p < PH_N; ++p) h->ev_used[p] = false;
   *out = h;
   return MQ_OK;
 }
 
 int mq_destroy(mq_handle* h) {
   if (!h) return MQ_OK;
-  if (h->ev_made)
-    for (int p = 0; p < PH_N; ++p) { (void)hipEventDestroy(h->ev0[p]); (void)hipEventDestroy(h->ev1[p]); }
+  for (auto e : h->ev0) (void)hipEventDestroy(e);
+  for (auto e : h->ev1) (void)hipEventDestroy(e);
   if (h->ws) (void)hipFree(h->ws);
   delete h;
   return MQ_OK;
@@ -378,14 +396,14 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
     MQ_HIP(launch_gemm(p, d.NH, d.S, ns, s));
   }
   pt.begin(PH_RED);
-  if ((rc = reduce_into(w.slab_fc1, h->nsplit_fc1, (int64_t)mq::H * d.I + mq::H, h->grad + h->off[MQ_P_FC1_W], s)))
+  if ((rc = reduce_into(w.slab_fc1, h->nsplit_fc1, (int64_t)mq::H * d.I + mq::H, h->grad + h->off[MQ_P_FC1_W], w.red_tmp, s)))
     return rc;
-  if ((rc = reduce_into(w.slab_rnn, h->nblk_bwd, h->len_rnn, h->grad + h->off[MQ_P_RNN_W_IH], s))) return rc;
+  if ((rc = reduce_into(w.slab_rnn, h->nblk_bwd, h->len_rnn, h->grad + h->off[MQ_P_RNN_W_IH], w.red_tmp, s))) return rc;
   if (c.mixer == MQ_MIXER_QMIX) {
-    if ((rc = reduce_into(w.slab_mix, h->nsplit_mix, h->len_mix, h->grad + h->off[MQ_P_HW1_W], s))) return rc;
-    if ((rc = reduce_into(w.slab_v2, h->nblk_mix, d.E + 1, h->grad + h->off[MQ_P_V2_W], s))) return rc;
+    if ((rc = reduce_into(w.slab_mix, h->nsplit_mix, h->len_mix, h->grad + h->off[MQ_P_HW1_W], w.red_tmp, s))) return rc;
+    if ((rc = reduce_into(w.slab_v2, h->nblk_mix, d.E + 1, h->grad + h->off[MQ_P_V2_W], w.red_tmp, s))) return rc;
   }
-  if ((rc = reduce_into(w.loss_part, h->nblk_mix, MQ_NSUMS, h->grad + h->P, s))) return rc;
+  if ((rc = reduce_into(w.loss_part, h->nblk_mix, MQ_NSUMS, h->grad + h->P, w.red_tmp, s))) return rc;
   pt.end();
   h->last = d;
   h->have_fb = true;
@@ -407,6 +425,7 @@ int mq_apply(mq_handle* h, void* stream) {
                      (const float*)h->w.norm_part, kNormBlocks, hp, h->stats);
   MQ_HIP(hipGetLastError());
   pt.end();
+  ++h->tstep;
   return MQ_OK;
 }
 
@@ -489,17 +508,20 @@ int mq_greedy_actions(const float* q, const int32_t* avail, int64_t* out, int32_
   return MQ_OK;
 }
 
-int mq_set_timing(mq_handle* h, int32_t on) {
-  if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
-  if (on && !h->ev_made) {
-    for (int p = 0; p < PH_N; ++p) {
-      MQ_HIP(hipEventCreate(&h->ev0[p]));
-      MQ_HIP(hipEventCreate(&h->ev1[p]));
-    }
-    h->ev_made = true;
+int mq_set_timing(mq_handle* h, int32_t slots, uint32_t phase_mask) {
+  if (!h || slots < 0 || slots > 4096) return set_err(MQ_ERR_ARG, "bad mq_set_timing args");
+  for (auto e : h->ev0) (void)hipEventDestroy(e);
+  for (auto e : h->ev1) (void)hipEventDestroy(e);
+  h->ev0.clear(); h->ev1.clear(); h->ev_used.clear();
+  h->slots = slots;
+  h->mask = phase_mask;
+  h->tstep = 0;
+  const size_t n = (size_t)slots * PH_N;
+  h->ev0.resize(n); h->ev1.resize(n); h->ev_used.assign(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    MQ_HIP(hipEventCreate(&h->ev0[i]));
+    MQ_HIP(hipEventCreate(&h->ev1[i]));
   }
-  h->timing = on != 0;
-  for (int p = 0; p < PH_N; ++p) h->ev_used[p] = false;
   return MQ_OK;
 }
 
@@ -507,11 +529,18 @@ int mq_phase_times(mq_handle* h, float* ms, int32_t cap, int32_t* n) {
   if (!h || !ms) return set_err(MQ_ERR_ARG, "NULL argument");
   if (n) *n = PH_N;
   for (int p = 0; p < PH_N && p < cap; ++p) {
-    ms[p] = 0.0f;
-    if (h->ev_made && h->ev_used[p]) {
-      MQ_HIP(hipEventSynchronize(h->ev1[p]));
-      MQ_HIP(hipEventElapsedTime(&ms[p], h->ev0[p], h->ev1[p]));
+    double sum = 0.0;
+    int cnt = 0;
+    for (int sl = 0; sl < h->slots; ++sl) {
+      const size_t i = (size_t)sl * PH_N + p;
+      if (!h->ev_used[i]) continue;
+      float t = 0.0f;
+      MQ_HIP(hipEventSynchronize(h->ev1[i]));
+      MQ_HIP(hipEventElapsedTime(&t, h->ev0[i], h->ev1[i]));
+      sum += t;
+      ++cnt;
     }
+    ms[p] = cnt ? (float)(sum / cnt) : 0.0f;
   }
   return MQ_OK;
 }

@@ -6,14 +6,25 @@
 
 namespace mq {
 
-// dst[i] = sum_z slab[z*len + i], z in order (bitwise reproducible).
+// dst[blockIdx.y*len + i] = sum over z in [y*zc, min(nslab, (y+1)*zc)) of slab[z*len + i], z ascending.
+// With gridDim.y == 1 this is the whole reduction; larger slab counts go through two passes (zc = 16, then the
+// partials) so thousands of workgroups keep 16 independent loads each in flight. Fixed order: bitwise
+// reproducible.
+constexpr int kRedZ = 16;
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restrict__ slab, int nslab, int64_t len,
-                                                           float* __restrict__ dst) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < len; i += (int64_t)gridDim.x * 256) {
-    float s = 0.0f;
-    for (int z = 0; z < nslab; ++z) s += slab[(int64_t)z * len + i];
-    dst[i] = s;
+                                                           int zc, float* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= len) return;
+  const int z0 = blockIdx.y * zc, z1 = min(nslab, z0 + zc);
+  float v[kRedZ];
+  float s = 0.0f;
+  for (int zb = z0; zb < z1; zb += kRedZ) {
+#pragma unroll
+    for (int u = 0; u < kRedZ; ++u) v[u] = (zb + u < z1) ? slab[(int64_t)(zb + u) * len + i] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < kRedZ; ++u) s += v[u];
   }
+  dst[(int64_t)blockIdx.y * len + i] = s;
 }
 
 // Per-block partial sum of squares of the (unnormalised) gradient.

@@ -22,6 +22,7 @@ from torch.optim import RMSprop
 from .. import _lib
 from ..components.episode_buffer import SampledBatch
 from ..modules.flat import pack, rebind
+from .dp import allreduce_grad_buffer
 from ..modules.mixers.qmix import QMixer
 from ..modules.mixers.vdn import VDNMixer
 
@@ -204,9 +205,7 @@ class QLearner:
         lib, s = h.lib, _lib.stream_ptr()
         _lib.check(lib.mq_forward_backward(h.h, ctypes.byref(rep), s))
         if self.dp:
-            import torch.distributed as dist
-            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-                dist.all_reduce(self._grad)
+            allreduce_grad_buffer(self._grad)
         _lib.check(lib.mq_apply(h.h, s))
         self._opt_steps += 1
         for p in self.params:
@@ -297,9 +296,12 @@ class QLearner:
             return out.view(Tp, B, n, A).permute(1, 0, 2, 3)
         return out.view(Tp - 1, B, n).permute(1, 0, 2)
 
-    def set_timing(self, on=True):
+    def set_timing(self, slots=1, phases=None):
+        """Record HIP events around the named phases (None = all) for the next `slots` steps (0 = off)."""
         h = self._handle
-        _lib.check(h.lib.mq_set_timing(h.h, int(on)))
+        names = h.lib.mq_phase_names().decode().split(";")
+        mask = 0xFFFFFFFF if phases is None else sum(1 << names.index(p) for p in phases)
+        _lib.check(h.lib.mq_set_timing(h.h, int(slots), mask))
 
     def phase_times(self):
         h = self._handle
@@ -308,3 +310,6 @@ class QLearner:
         _lib.check(h.lib.mq_phase_times(h.h, ms, 32, ctypes.byref(n)))
         names = h.lib.mq_phase_names().decode().split(";")
         return {names[i]: ms[i] for i in range(n.value)}
+
+    def phase_names(self):
+        return _lib.load().mq_phase_names().decode().split(";")

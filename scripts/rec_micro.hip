@@ -1,0 +1,62 @@
+// Microbenchmark of the persistent GRU recurrence kernels at a given (B, n, T) with random data.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/rec_micro.hip -o /tmp/rec_micro && /tmp/rec_micro 32 8 120
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "../pymarl_amd/csrc/gru_kernels.hpp"
+using namespace mq;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
+
+template <class F> float time_it(F f, int reps = 20) {
+  hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  f(); CK(hipDeviceSynchronize());
+  CK(hipEventRecord(a));
+  for (int i = 0; i < reps; ++i) f();
+  CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+  float ms; CK(hipEventElapsedTime(&ms, a, b));
+  return ms / reps * 1000.0f;   // us
+}
+
+float* dev_rand(size_t n, float scale) {
+  std::vector<float> h(n);
+  for (auto& x : h) x = scale * ((rand() / (float)RAND_MAX) * 2.0f - 1.0f);
+  float* d; CK(hipMalloc(&d, n * 4)); CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+  return d;
+}
+
+int main(int argc, char** argv) {
+  int B = argc > 1 ? atoi(argv[1]) : 32, n = argc > 2 ? atoi(argv[2]) : 8, T = argc > 3 ? atoi(argv[3]) : 120;
+  int A = 14, O = 80;
+  Dims d{};
+  d.n = n; d.A = A; d.O = O; d.S = 168; d.E = 32; d.I = O + A + n; d.NH = 32 * (n + 3);
+  d.B = B; d.Tp = T + 1; d.T = T; d.R = B * n; d.M = T * B; d.t_stride = T + 1;
+  d.last_action = 1; d.agent_id = 1; d.mixer = 2; d.double_q = 1; d.gamma = 0.99f;
+  d.dR = make_fastdiv(d.R); d.dN = make_fastdiv(n); d.dB = make_fastdiv(B);
+  const int64_t RT = (int64_t)d.Tp * d.R;
+  Lay L{};
+  int64_t o = 0, sz[MQ_P_COUNT] = {};
+  sz[MQ_P_FC1_W] = 64 * d.I; sz[MQ_P_FC1_B] = 64; sz[MQ_P_RNN_W_IH] = 192 * 64; sz[MQ_P_RNN_W_HH] = 192 * 64;
+  sz[MQ_P_RNN_B_IH] = 192; sz[MQ_P_RNN_B_HH] = 192; sz[MQ_P_FC2_W] = A * 64; sz[MQ_P_FC2_B] = A;
+  for (int i = 0; i < MQ_P_COUNT; ++i) { L.o[i] = o; o += sz[i]; }
+  L.o[MQ_P_COUNT] = o;
+  float* P0 = dev_rand(o, 0.12f);
+  float* P1 = dev_rand(o, 0.12f);
+  Work w{};
+  w.GI = dev_rand(2 * RT * 192, 1.0f);
+  CK(hipMalloc(&w.Hs, RT * 64 * 4)); CK(hipMalloc(&w.Gates, RT * 256 * 4)); CK(hipMalloc(&w.Q, 2 * RT * A * 4));
+  auto run = [&](auto kern, int rw) {
+    dim3 grid((d.R + rw - 1) / rw, 2);
+    return time_it([&] { hipLaunchKernelGGL(kern, grid, dim3(256), 0, 0, d, (const float*)P0, (const float*)P1, L, w); });
+  };
+  printf("B=%d n=%d T=%d rows=%d\n", B, n, T, d.R);
+  printf("fwd RW1 V0 %.1f us\n", run(gru_fwd_kernel<1, 0>, 1));
+  printf("fwd RW1 V1(no Hs/Gates st) %.1f us\n", run(gru_fwd_kernel<1, 1>, 1));
+  printf("fwd RW1 V2(no fc2) %.1f us\n", run(gru_fwd_kernel<1, 2>, 1));
+  printf("fwd RW1 V3(no st, no fc2) %.1f us\n", run(gru_fwd_kernel<1, 3>, 1));
+  printf("fwd RW1 V4(no prefetch) %.1f us\n", run(gru_fwd_kernel<1, 4>, 1));
+  printf("fwd RW1 V7(none) %.1f us\n", run(gru_fwd_kernel<1, 7>, 1));
+  printf("fwd RW2 V0 %.1f us\n", run(gru_fwd_kernel<2, 0>, 2));
+  printf("fwd RW4 V0 %.1f us\n", run(gru_fwd_kernel<4, 0>, 4));
+  return 0;
+}

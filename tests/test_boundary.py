@@ -1,0 +1,76 @@
+"""The C-ABI boundary: libmq_learner.so loads on CPU and exports every symbol include/mq_learner.h declares; the
+ctypes structs match the C layout (checked by compiling a probe against the header with gcc); argument
+validation errors surface as the reference's exception types without touching the GPU."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from pymarl_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mq_learner.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(mq_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    decl = declared_functions()
+    assert len(decl) >= 15
+    for name in decl:
+        assert hasattr(lib, name), name
+    assert sorted(_lib.EXPORTS) == decl
+
+
+def test_ctypes_struct_layout_matches_header(tmp_path):
+    src = tmp_path / "probe.c"
+    src.write_text("""
+#include <stdio.h>
+#include <stddef.h>
+#include "mq_learner.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu\\n", sizeof(mq_config), offsetof(mq_config, gamma), offsetof(mq_config, max_seq),
+         sizeof(mq_replay), offsetof(mq_replay, batch_size));
+  printf("%d %d\\n", MQ_P_COUNT, MQ_NSUMS);
+  return 0;
+}
+""")
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    c = [int(x) for x in out]
+    py = [ctypes.sizeof(_lib.MQConfig), _lib.MQConfig.gamma.offset, _lib.MQConfig.max_seq.offset,
+          ctypes.sizeof(_lib.MQReplay), _lib.MQReplay.batch_size.offset, _lib.P_COUNT, _lib.NSUMS]
+    assert c == py
+
+
+def test_unknown_mixer_is_value_error_before_any_hip_call():
+    lib = _lib.load()
+    cfg = _lib.MQConfig(n_agents=3, n_actions=9, obs_dim=30, state_dim=48, rnn_hidden_dim=64, mixing_embed_dim=32,
+                        mixer=7, max_batch=4, max_seq=11)
+    h = ctypes.c_void_p()
+    rc = lib.mq_create(ctypes.byref(cfg), ctypes.byref(h))
+    assert rc == 1
+    with pytest.raises(ValueError, match="not recognised"):
+        _lib.check(rc)
+
+
+def test_config_validation():
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    bad = _lib.MQConfig(n_agents=3, n_actions=9, obs_dim=30, state_dim=48, rnn_hidden_dim=32, mixing_embed_dim=32,
+                        mixer=2, max_batch=4, max_seq=11)
+    assert lib.mq_create(ctypes.byref(bad), ctypes.byref(h)) == 1
+    assert b"rnn_hidden_dim" in lib.mq_last_error()
+
+
+def test_train_without_handle_bound_reports_state_error():
+    lib = _lib.load()
+    assert lib.mq_apply(None, None) != 0
+    assert lib.mq_forward_backward(None, None, None) != 0

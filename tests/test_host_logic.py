@@ -1,0 +1,148 @@
+"""Host-side mirror of the reference interfaces (CPU): EpisodeBatch / ReplayBuffer semantics, SampledBatch
+zero-copy views, parameter packing and checkpoint compatibility, and the no-CPU-fallback rule."""
+import logging
+import os
+from types import SimpleNamespace as SN
+
+import numpy as np
+import pytest
+import torch as th
+
+from pymarl_amd import _lib
+from pymarl_amd.components.episode_buffer import EpisodeBatch, ReplayBuffer, SampledBatch
+from pymarl_amd.components.transforms import OneHot
+from pymarl_amd.controllers import REGISTRY as mac_REGISTRY
+from pymarl_amd.learners import REGISTRY as le_REGISTRY
+from pymarl_amd.utils.logging import Logger
+from pymarl_amd.utils.synthetic import agent_param_shapes, qmix_param_shapes
+
+
+def scheme(O=3, A=5, S=4):
+    return {
+        "state": {"vshape": S},
+        "obs": {"vshape": O, "group": "agents"},
+        "actions": {"vshape": (1,), "group": "agents", "dtype": th.long},
+        "avail_actions": {"vshape": (A,), "group": "agents", "dtype": th.int},
+        "reward": {"vshape": (1,)},
+        "terminated": {"vshape": (1,), "dtype": th.uint8},
+    }
+
+
+def args(mixer="qmix", n=2, A=5, O=3, S=4):
+    return SN(n_agents=n, n_actions=A, state_shape=S, obs_shape=O, rnn_hidden_dim=64, mixing_embed_dim=32,
+              mixer=mixer, lr=5e-4, optim_alpha=0.99, optim_eps=1e-5, grad_norm_clip=10.0, gamma=0.99,
+              double_q=True, target_update_interval=200, learner_log_interval=0, obs_last_action=True,
+              obs_agent_id=True, agent="rnn", mac="basic_mac", agent_output_type="q",
+              action_selector="epsilon_greedy", epsilon_start=1.0, epsilon_finish=0.05, epsilon_anneal_time=50000,
+              batch_size=3, device="cpu")
+
+
+def test_episode_batch_update_and_onehot_preprocess():
+    pre = {"actions": ("actions_onehot", [OneHot(out_dim=5)])}
+    eb = EpisodeBatch(scheme(), {"agents": 2}, 4, 3, preprocess=pre)
+    eb.update({"actions": th.ones(2, 1).long(), "obs": th.ones(2, 3), "state": th.ones(4)}, 0, 0)
+    assert eb["filled"][0, 0, 0] == 1 and eb["filled"][1, 0, 0] == 0
+    assert th.equal(eb["actions_onehot"][0, 0], th.tensor([[0, 1., 0, 0, 0]] * 2))
+    with pytest.raises(KeyError):
+        eb.update({"nope": th.ones(1)}, 0, 0)
+    with pytest.raises(ValueError):
+        eb["nope"]
+    sub = eb[1:3, :2]
+    assert sub.batch_size == 2 and sub.max_seq_length == 2 and sub["obs"].shape == (2, 2, 2, 3)
+
+
+def test_replay_buffer_wraparound_and_lengths():
+    pre = {"actions": ("actions_onehot", [OneHot(out_dim=5)])}
+    rb = ReplayBuffer(scheme(), {"agents": 2}, 5, 3, preprocess=pre)
+    eb = EpisodeBatch(scheme(), {"agents": 2}, 4, 3, preprocess=pre)
+    for t in range(2):
+        eb.update({"obs": th.full((4, 2, 3), float(t))}, ts=t)
+    rb.insert_episode_batch(eb)
+    rb.insert_episode_batch(eb)   # 4 + 4 > 5: wraps (episode_buffer.py:283-286)
+    assert rb.episodes_in_buffer == 5 and rb.buffer_index == 3
+    assert list(rb.episode_lengths) == [2, 2, 2, 2, 2]
+
+
+def test_sample_matches_reference_rng_and_gather():
+    rb = ReplayBuffer(scheme(), {"agents": 2}, 10, 4)
+    rb.load_arrays({"obs": np.arange(10 * 4 * 2 * 3, dtype=np.float32).reshape(10, 4, 2, 3),
+                    "filled": np.ones((10, 4, 1), dtype=np.int64)})
+    np.random.seed(5)
+    s = rb.sample(3)
+    np.random.seed(5)
+    ids = np.random.choice(10, 3, replace=False)      # episode_buffer.py:297
+    assert isinstance(s, SampledBatch) and np.array_equal(s.ep_ids_np, ids)
+    assert th.equal(s["obs"], rb["obs"][th.as_tensor(ids)])
+    s2 = s[:, :2]
+    assert s2.t_len == 2 and s2["obs"].shape == (3, 2, 2, 3) and s2.max_t_filled() == 2
+    assert th.equal(s2.materialize()["obs"], rb["obs"][th.as_tensor(ids)][:, :2])
+    sh = s.shard(1, 2)
+    assert np.array_equal(sh.ep_ids_np, ids[1:3])
+    full = ReplayBuffer(scheme(), {"agents": 2}, 3, 4)
+    full.load_arrays({"filled": np.ones((3, 4, 1), dtype=np.int64)})
+    st = np.random.get_state()
+    assert np.array_equal(full.sample(3).ep_ids_np, np.arange(3))   # no RNG draw (episode_buffer.py:293-294)
+    assert np.random.get_state()[2] == st[2]
+
+
+def build_cpu(mixer="qmix"):
+    a = args(mixer)
+    sch = scheme()
+    rb = ReplayBuffer(sch, {"agents": 2}, 4, 3, preprocess={"actions": ("actions_onehot", [OneHot(5)])})
+    mac = mac_REGISTRY["basic_mac"](rb.scheme, {"agents": 2}, a)
+    learner = le_REGISTRY["q_learner"](mac, rb.scheme, Logger(logging.getLogger("t")), a)
+    return a, rb, mac, learner
+
+
+def test_parameter_names_order_and_flat_layout():
+    a, rb, mac, learner = build_cpu()
+    I = 3 + 5 + 2
+    want = list(agent_param_shapes(I, 64, 5).items())
+    got = [(k, tuple(v.shape)) for k, v in mac.agent.state_dict().items()]
+    assert got == [(k, tuple(s)) for k, s in want]
+    mix = [(k, tuple(v.shape)) for k, v in learner.mixer.state_dict().items()]
+    assert mix == [(k, tuple(s)) for k, s in qmix_param_shapes(4, 2, 32).items()]
+    # every parameter is a view into the one flat buffer, in MQ_P_* order
+    o = 0
+    for p in learner.params:
+        assert p.data_ptr() == learner._online.data_ptr() + 4 * o
+        o += p.numel()
+    assert o == learner.n_params
+    assert learner.target_mac.agent.fc1.weight.data_ptr() == learner._target.data_ptr()
+    with th.no_grad():
+        learner.mixer.hyper_b_1.bias.fill_(3.0)
+    assert learner._online[learner.n_params - 1 - 1 - 32 - 32 * 4 - 32: learner.n_params].max() == 3.0
+
+
+def test_unknown_mixer_raises_value_error():
+    a = args("foo")
+    rb = ReplayBuffer(scheme(), {"agents": 2}, 4, 3, preprocess={"actions": ("actions_onehot", [OneHot(5)])})
+    mac = mac_REGISTRY["basic_mac"](rb.scheme, {"agents": 2}, a)
+    with pytest.raises(ValueError, match="Mixer foo not recognised"):
+        le_REGISTRY["q_learner"](mac, rb.scheme, Logger(logging.getLogger("t")), a)
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    a, rb, mac, learner = build_cpu()
+    with th.no_grad():
+        learner._online.normal_()
+        learner._sq.uniform_()
+    learner.save_models(str(tmp_path))
+    assert sorted(os.listdir(tmp_path)) == ["agent.th", "mixer.th", "opt.th"]
+    sd = th.load(tmp_path / "opt.th", weights_only=True)
+    assert len(sd["state"]) == len(learner.params) and "square_avg" in sd["state"][0]
+    a2, rb2, mac2, learner2 = build_cpu()
+    learner2.load_models(str(tmp_path))
+    assert th.equal(learner2._online, learner._online)
+    assert th.equal(learner2._sq, learner._sq)
+    Pa = sum(p.numel() for p in learner.mac.agent.parameters())
+    # target agent reloads from the online agent.th; the target mixer is not reloaded (q_learner.py:137-143)
+    assert th.equal(learner2._target[:Pa], learner._online[:Pa])
+    assert learner2.mac.agent.fc1.weight.data_ptr() == learner2._online.data_ptr()
+
+
+def test_no_cpu_fallback():
+    a, rb, mac, learner = build_cpu("vdn")
+    rb.load_arrays({"filled": np.ones((4, 3, 1), dtype=np.int64)})
+    with pytest.raises(_lib.MQError, match="no CPU"):
+        learner.train(rb.sample(3), 0, 0)
