@@ -56,7 +56,8 @@ def algorithmic_flops(phase, n, A, O, S, T, B, E=32, H=64, mixer="qmix"):
     f = {
         "fc1": 2 * 2 * RT * H * O,                          # both nets, obs part (one-hot columns are gathers)
         "gi": 2 * 2 * RT * 3 * H * H,                       # both nets
-        "gru_fwd": 2 * 2 * RT * (3 * H * H + H * A),        # W_hh mat-vec + fc2, both nets
+        "gru_fwd": 2 * 2 * RT * 3 * H * H,                  # W_hh mat-vec, both nets
+        "fc2": 2 * 2 * RT * H * A,
         "hyper": 2 * 2 * M * NH * S if mixer == "qmix" else 0,
         "gru_bwd": 2 * RT * (3 * H * H) * 3,                # W_hh^T mat-vec + dW_hh + dW_ih accumulations
         "dx1": 2 * RT * 3 * H * H,

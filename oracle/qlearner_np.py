@@ -196,8 +196,12 @@ class OracleQLearner:
         self.log_stats_t = -self.cfg.get("learner_log_interval", 0) - 1
         self.last = {}
 
-    def forward(self, batch, keep_cache=False):
-        """q_learner.py:39-97: returns dict of intermediates (+ caches)."""
+    def forward(self, batch, keep_cache=False, cur_max_override=None):
+        """q_learner.py:39-97: returns dict of intermediates (+ caches).
+
+        cur_max_override (B, T, n): use these double-Q argmax actions instead of recomputing them — lets a parity
+        test follow the other implementation through near-tie argmax flips (both choices are correct fp32 ties).
+        """
         c = self.cfg
         n = c["n_agents"]
         rewards = batch["reward"][:, :-1].astype(F32)
@@ -215,6 +219,8 @@ class OracleQLearner:
             mod = mac_out.copy()
             mod[avail == 0] = NEG
             cur_max = mod[:, 1:].argmax(axis=3)
+            if cur_max_override is not None:
+                cur_max = np.asarray(cur_max_override, dtype=np.int64)
             target_max = np.take_along_axis(tmo, cur_max[..., None], axis=3)[..., 0]
         else:
             cur_max = tmo.argmax(axis=3)
@@ -238,10 +244,10 @@ class OracleQLearner:
                     target_max=target_max, q_tot=q_tot, target_q_tot=tq_tot, targets=targets, td=td, mask=m,
                     mask_sum=msum, loss=float(loss), acache=acache, mcache=mcache, actions=actions)
 
-    def gradients(self, batch, fw=None):
+    def gradients(self, batch, fw=None, cur_max_override=None):
         """Unclipped gradients of the loss (agent params then mixer params, reference order)."""
         c = self.cfg
-        fw = fw or self.forward(batch, keep_cache=True)
+        fw = fw or self.forward(batch, keep_cache=True, cur_max_override=cur_max_override)
         td, m, msum = fw["td"], fw["mask"], fw["mask_sum"]
         dq_tot = ((F32(2.0) * (td * m)) * (F32(1.0) / msum)) * m            # d/dQ_tot of sum((td*m)^2)/sum(m)
         B, T = td.shape[:2]
@@ -262,10 +268,10 @@ class OracleQLearner:
         ag = agent_backward(self.p, fw["acache"], dmac)
         return ag, mg, fw
 
-    def train(self, batch, t_env, episode_num):
+    def train(self, batch, t_env, episode_num, cur_max_override=None):
         """q_learner.py:37-116; returns the stats dict it would log."""
         c = self.cfg
-        ag, mg, fw = self.gradients(batch)
+        ag, mg, fw = self.gradients(batch, cur_max_override=cur_max_override)
         grads = OrderedDict(list(ag.items()) + list(mg.items()))
         grad_norm = clip_grad_norm(grads, c["grad_norm_clip"])
         params = OrderedDict(list(self.p.items()) + list(self.mp.items()))

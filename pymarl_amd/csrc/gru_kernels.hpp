@@ -3,11 +3,20 @@
 // Only the h -> h dependency is serial: the input side (fc1, W_ih) was hoisted into the row-parallel GEMMs, so
 // each step here is the 64x192 W_hh mat-vec plus gate math (forward) or its transpose plus the gate
 // derivatives (backward). A workgroup owns RW rows for the whole T loop; W_hh stays in VGPRs and the hidden /
-// gate-gradient vectors round-trip through double-buffered LDS, one barrier per step.
+// gate-gradient vectors round-trip through double-buffered LDS, one LDS-only barrier per step.
 //
 // Thread map (256 threads): unit j = tid >> 2 (0..63), quarter q = tid & 3. The four lanes of a quad hold the
 // four K-quarters of one hidden unit and meet in a DPP quad reduction (no LDS). Gate math for row i runs on the
-// lane with q == i % 4, so RW = 4 keeps every lane busy.
+// lane with q == i % 4.
+//
+// Latency structure of one step (what the code is arranged around):
+//  * the step's global inputs are prefetched one step ahead into one of two register sets; the T loop is
+//    unrolled by two so the sets swap roles without register moves at the loop latch (a move would force a
+//    vmcnt wait that, counters being in-order on gfx950, also waits for the step's output stores);
+//  * forward: the loop is VALU-issue bound (two waves per SIMD), so everything not on the h chain is out of
+//    it: fc2 runs afterwards as a row-parallel GEMM over the stored hidden states of both nets;
+//  * backward: W2 is staged in LDS so the dchosen -> dh term is an LDS gather, and the per-row replay
+//    addressing (episode id -> action row) is resolved once before the loop.
 #pragma once
 #include "learner_types.hpp"
 
@@ -25,18 +34,24 @@ MQ_DEV float pick_row(const float (&v)[RW], int ii, int q) {
   return out;
 }
 
+// tanh(x) = 1 - 2 / (1 + e^{2x}): one v_exp + one v_rcp; absolute error ~1e-7 (relative error grows only where
+// |tanh| < 1e-3, where the absolute error is what enters h).
+MQ_DEV float tanh_fast(float x) {
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(2.8853900817779268f * x));
+}
+
+MQ_DEV float sigm_fast(float x) {   // 1 / (1 + e^-x) with v_exp_f32 / v_rcp_f32
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
+
 // ------------------------------------------------------------------------------------------------ forward
-// grid = (ceil(R / RW), 2 nets). Writes Q for both nets; Hs and Gates for the online net only.
-// VAR: ablation bits for scripts/rec_micro.hip only (production = 0): 1 skip Hs/Gates stores, 2 skip fc2,
-// 4 skip the GI prefetch (load at use).
-template <int RW, int VAR = 0>
-__global__ __launch_bounds__(256) void gru_fwd_kernel(Dims d, const float* __restrict__ P0,
-                                                      const float* __restrict__ P1, Lay L, Work w) {
-  constexpr int RL = (RW + 3) / 4;   // rows per lane in the gate phase
-  const int z = blockIdx.y;
-  const float* __restrict__ P = z ? P1 : P0;
+// VAR: ablation bits for scripts/rec_micro.hip only (production = 0): 1 skip Hs/Gates stores,
+// 2 stamp the T loop (cycles, 100 MHz ticks) into w.slab_mix.
+template <int RW, bool ONLINE, int VAR>
+MQ_DEV void gru_fwd_body(const Dims& d, const float* __restrict__ P, const Lay& L, const Work& w, int z) {
+  constexpr int RL = (RW + 3) / 4;
   const int tid = threadIdx.x, j = tid >> 2, q = tid & 3;
-  const int R = d.R, A = d.A;
+  const int R = d.R, A = d.A, Tp = d.Tp;
   const int64_t RT = d.RT();
   __shared__ float hbuf[2][RW][H];
 
@@ -52,43 +67,31 @@ __global__ __launch_bounds__(256) void gru_fwd_kernel(Dims d, const float* __res
   }
   const float bhr = P[L.o[MQ_P_RNN_B_HH] + j], bhz = P[L.o[MQ_P_RNN_B_HH] + H + j],
               bhn = P[L.o[MQ_P_RNN_B_HH] + 2 * H + j];
-  // fc2 role: action a = j (< A), same quarter split of K.
-  const bool has_a = j < A;
-  float w2[16];
-  float b2 = 0.0f;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) w2[k] = has_a ? P[L.o[MQ_P_FC2_W] + j * H + 16 * q + k] : 0.0f;
-  if (has_a) b2 = P[L.o[MQ_P_FC2_B] + j];
 
   const int r0 = blockIdx.x * RW;
+  int rr[RL];
+  bool rv[RL];
+#pragma unroll
+  for (int ii = 0; ii < RL; ++ii) {
+    const int i = 4 * ii + q, r = r0 + i;
+    rv[ii] = i < RW && r < R;
+    rr[ii] = min(r, R - 1);
+  }
   for (int i = tid; i < RW * H; i += 256) hbuf[0][i / H][i % H] = 0.0f;   // init_hidden: h0 = 0
 
   const float* GI = w.GI + (int64_t)z * RT * G3;
-  float* Q = w.Q + (int64_t)z * RT * A;
-  float gi_r[RL], gi_z[RL], gi_n[RL];
-  auto load_gi = [&](int t) {
+  float* Hz = w.Hs + (int64_t)z * RT * H;
+  auto load = [&](int t, float (&g)[RL][3]) {
+    const int tc = min(t, Tp - 1);
 #pragma unroll
     for (int ii = 0; ii < RL; ++ii) {
-      const int i = 4 * ii + q, r = r0 + i;
-      if (i < RW && r < R && t < d.Tp) {
-        const float* g = GI + ((int64_t)t * R + r) * G3;
-        gi_r[ii] = g[j]; gi_z[ii] = g[H + j]; gi_n[ii] = g[2 * H + j];
-      } else {
-        gi_r[ii] = gi_z[ii] = gi_n[ii] = 0.0f;
-      }
+      const float* p = GI + ((int64_t)tc * R + rr[ii]) * G3;
+      g[ii][0] = p[j]; g[ii][1] = p[H + j]; g[ii][2] = p[2 * H + j];
     }
   };
-  load_gi(0);
-  drain_vmem();
-  lds_barrier();
-
-  for (int t = 0; t < d.Tp; ++t) {
-    float cr[RL], cz[RL], cn[RL];
-#pragma unroll
-    for (int ii = 0; ii < RL; ++ii) { cr[ii] = gi_r[ii]; cz[ii] = gi_z[ii]; cn[ii] = gi_n[ii]; }
-    if (!(VAR & 4)) load_gi(t + 1);   // prefetch the next step's input gates under this step's mat-vec
-
-    float (*hb)[H] = hbuf[t & 1];
+  auto step = [&](int t, const float (&cur)[RL][3], float (&nxt)[RL][3]) {
+    load(t + 1, nxt);   // next step's input gates, in flight under this step
+    const float (*hb)[H] = hbuf[t & 1];
     float (*hn)[H] = hbuf[(t + 1) & 1];
     float sr[RW], sz[RW], sn[RW];
 #pragma unroll
@@ -98,12 +101,13 @@ __global__ __launch_bounds__(256) void gru_fwd_kernel(Dims d, const float* __res
 #pragma unroll
       for (int k4 = 0; k4 < 4; ++k4) {
         const f32x4 hv = hv4[k4];
-        ar = fmaf(wr[4 * k4 + 0], hv[0], ar); ar2 = fmaf(wr[4 * k4 + 1], hv[1], ar2);
-        az = fmaf(wz[4 * k4 + 0], hv[0], az); az2 = fmaf(wz[4 * k4 + 1], hv[1], az2);
-        an = fmaf(wn[4 * k4 + 0], hv[0], an); an2 = fmaf(wn[4 * k4 + 1], hv[1], an2);
-        ar = fmaf(wr[4 * k4 + 2], hv[2], ar); ar2 = fmaf(wr[4 * k4 + 3], hv[3], ar2);
-        az = fmaf(wz[4 * k4 + 2], hv[2], az); az2 = fmaf(wz[4 * k4 + 3], hv[3], az2);
-        an = fmaf(wn[4 * k4 + 2], hv[2], an); an2 = fmaf(wn[4 * k4 + 3], hv[3], an2);
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const int k = 4 * k4 + e;
+          ar = fmaf(wr[k], hv[e], ar); ar2 = fmaf(wr[k + 1], hv[e + 1], ar2);
+          az = fmaf(wz[k], hv[e], az); az2 = fmaf(wz[k + 1], hv[e + 1], az2);
+          an = fmaf(wn[k], hv[e], an); an2 = fmaf(wn[k + 1], hv[e + 1], an2);
+        }
       }
       sr[i] = quad_sum(ar + ar2);
       sz[i] = quad_sum(az + az2);
@@ -111,64 +115,81 @@ __global__ __launch_bounds__(256) void gru_fwd_kernel(Dims d, const float* __res
     }
 #pragma unroll
     for (int ii = 0; ii < RL; ++ii) {
-      const int i = 4 * ii + q, r = r0 + i;
+      const int i = 4 * ii + q;
       const float ghr = pick_row<RW>(sr, ii, q) + bhr;
       const float ghz = pick_row<RW>(sz, ii, q) + bhz;
       const float ghn = pick_row<RW>(sn, ii, q) + bhn;
       if (i < RW) {
         const float hp = hb[i][j];
-        const float rg = sigmoidf_(ghr + cr[ii]);
-        const float zg = sigmoidf_(ghz + cz[ii]);
-        const float ng = tanhf_(cn[ii] + ghn * rg);
+        const float rg = sigm_fast(ghr + cur[ii][0]);
+        const float zg = sigm_fast(ghz + cur[ii][1]);
+        const float ng = tanh_fast(cur[ii][2] + ghn * rg);
         const float h1 = (hp - ng) * zg + ng;   // ATen gru_cell: (hx - n) * z + n
         hn[i][j] = h1;
-        if (!(VAR & 1) && z == 0 && r < R) {
-          const int64_t tr = (int64_t)t * R + r;
-          w.Hs[tr * H + j] = h1;
-          float* g = w.Gates + tr * (4 * H);
-          g[j] = rg; g[H + j] = zg; g[2 * H + j] = ng; g[3 * H + j] = ghn;
+        if (!(VAR & 1) && rv[ii]) {
+          const int64_t tr = (int64_t)t * R + rr[ii];
+          Hz[tr * H + j] = h1;   // both nets: fc2 runs afterwards as a row-parallel GEMM over H
+          if (ONLINE) {
+            float* g = w.Gates + tr * (4 * H);
+            g[j] = rg; g[H + j] = zg; g[2 * H + j] = ng; g[3 * H + j] = ghn;
+          }
         }
       }
     }
     lds_barrier();
-    if (VAR & 4) load_gi(t + 1);
-    // fc2 on the new hidden state: q = W2 h + b2 (rnn_agent.py:35)
-#pragma unroll
-    for (int i = 0; i < (VAR & 2 ? 0 : RW); ++i) {
-      const f32x4* hv4 = (const f32x4*)(&hn[i][16 * q]);
-      float s = 0.0f, s2 = 0.0f;
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) {
-        const f32x4 hv = hv4[k4];
-        s = fmaf(w2[4 * k4 + 0], hv[0], s); s2 = fmaf(w2[4 * k4 + 1], hv[1], s2);
-        s = fmaf(w2[4 * k4 + 2], hv[2], s); s2 = fmaf(w2[4 * k4 + 3], hv[3], s2);
-      }
-      s = quad_sum(s + s2);
-      const int r = r0 + i;
-      if (has_a && q == 0 && r < R) Q[((int64_t)t * R + r) * A + j] = s + b2;
-    }
+  };
+
+  float ga[RL][3], gb[RL][3];
+  load(0, ga);
+  drain_vmem();
+  lds_barrier();
+  uint64_t c0 = 0, r0t = 0;
+  if (VAR & 2) { c0 = __builtin_amdgcn_s_memtime(); r0t = __builtin_amdgcn_s_memrealtime(); }
+  int t = 0;
+  for (; t + 1 < Tp; t += 2) {
+    step(t, ga, gb);
+    step(t + 1, gb, ga);
   }
+  if (t < Tp) step(t, ga, gb);
+  if ((VAR & 2) && tid == 0) {   // diagnostic only: shader cycles and 100 MHz ticks of the whole T loop
+    const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    ((uint64_t*)w.slab_mix)[2 * (blockIdx.y * gridDim.x + blockIdx.x)] = c1 - c0;
+    ((uint64_t*)w.slab_mix)[2 * (blockIdx.y * gridDim.x + blockIdx.x) + 1] = r1 - r0t;
+  }
+}
+
+// grid = (ceil(R / RW), 2 nets). Writes Hs for both nets and Gates for the online net.
+template <int RW, int VAR = 0>
+__global__ __launch_bounds__(256) void gru_fwd_kernel(Dims d, const float* __restrict__ P0,
+                                                      const float* __restrict__ P1, Lay L, Work w) {
+  if (blockIdx.y == 0) gru_fwd_body<RW, true, VAR>(d, P0, L, w, 0);
+  else gru_fwd_body<RW, false, VAR>(d, P1, L, w, 1);
 }
 
 // ------------------------------------------------------------------------------------------------ backward
 // BPTT over the online net (q_learner.py:100-101). grid = ceil(R / RW). Writes dGI for the dX1 GEMM and a
 // per-workgroup partial slab [w_ih | w_hh | b_ih | b_hh | fc2.w | fc2.b] of the gradient.
-template <int RW>
+struct BwdIn {
+  float gr, gz, gn, ghn, hp, x1, dch;
+  int act;
+};
+
+template <int RW, int VAR = 0>
 __global__ __launch_bounds__(256) void gru_bwd_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
                                                       Work w, int64_t slab_len) {
   constexpr int RL = (RW + 3) / 4;
   const int tid = threadIdx.x, k = tid >> 2, q = tid & 3;
-  const int R = d.R, A = d.A;
+  const int R = d.R, A = d.A, T = d.T;
   __shared__ float dgh_s[2][RW][G3];
   __shared__ float dgi_s[2][RW][G3];
   __shared__ float hp_s[2][RW][H];
   __shared__ float x1_s[2][RW][H];
-  extern __shared__ float dyn[];   // dW2 partial [A][H] then db2 [A]
-  float* dw2_s = dyn;
-  float* db2_s = dyn + A * H;
+  extern __shared__ float dyn[];   // W2 [A][H] | dW2 partial [A][H] | db2 [A]
+  float* w2_s = dyn;
+  float* dw2_s = dyn + A * H;
+  float* db2_s = dyn + 2 * A * H;
 
   const float* Whh = P + L.o[MQ_P_RNN_W_HH];
-  const float* W2 = P + L.o[MQ_P_FC2_W];
   float wT[48], accH[48], accI[48];
 #pragma unroll
   for (int c = 0; c < 48; ++c) {
@@ -176,50 +197,72 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(Dims d, Rep rp, const floa
     accH[c] = 0.0f;
     accI[c] = 0.0f;
   }
-  for (int i = tid; i < A * H + A; i += 256) dyn[i] = 0.0f;
+  for (int i = tid; i < A * H; i += 256) { w2_s[i] = P[L.o[MQ_P_FC2_W] + i]; dw2_s[i] = 0.0f; }
+  for (int i = tid; i < A; i += 256) db2_s[i] = 0.0f;
 
   const int r0 = blockIdx.x * RW;
-  float carry[RL], cz[RL], ht[RL];
-  float dbi0 = 0, dbi1 = 0, dbi2 = 0, dbh2 = 0;
+  int rr[RL];
+  bool rv[RL];
+  const int64_t* arow[RL];   // &actions[ep(b)][0][agent], stride n per step
 #pragma unroll
-  for (int ii = 0; ii < RL; ++ii) { carry[ii] = 0.0f; cz[ii] = 0.0f; ht[ii] = 0.0f; }
-  drain_vmem();
-  lds_barrier();
-
-  for (int t = d.Tp - 1; t >= 0; --t) {
-    const int pb = t & 1;
-    int pa[RL];
-    float pv[RL], pd[RL];
+  for (int ii = 0; ii < RL; ++ii) {
+    const int i = 4 * ii + q, r = r0 + i;
+    rv[ii] = i < RW && r < R;
+    rr[ii] = min(r, R - 1);
+    const int b = (int)fdiv((uint32_t)rr[ii], d.dN), ag = rr[ii] - b * d.n;
+    arow[ii] = rp.actions + rp.ep(b) * d.t_stride * d.n + ag;
+  }
+  auto load = [&](int t, BwdIn (&s)[RL]) {
+    const int tc = max(t, 0);
+    const int td = min(tc, T - 1);
 #pragma unroll
     for (int ii = 0; ii < RL; ++ii) {
-      const int i = 4 * ii + q, r = r0 + i;
+      const int64_t tr = (int64_t)tc * R + rr[ii];
+      const float* g = w.Gates + tr * (4 * H);
+      s[ii].gr = g[k]; s[ii].gz = g[H + k]; s[ii].gn = g[2 * H + k]; s[ii].ghn = g[3 * H + k];
+      s[ii].hp = w.Hs[(tc > 0 ? tr - R : tr) * H + k];
+      s[ii].x1 = w.X1[tr * H + k];
+      s[ii].dch = w.dch[(int64_t)td * R + rr[ii]];
+      s[ii].act = (int)arow[ii][(int64_t)tc * d.n];
+    }
+  };
+
+  float carry[RL], ht[RL];
+  float dbi0 = 0, dbi1 = 0, dbi2 = 0, dbh2 = 0;
+#pragma unroll
+  for (int ii = 0; ii < RL; ++ii) { carry[ii] = 0.0f; ht[ii] = 0.0f; }
+
+  auto step = [&](int t, const BwdIn (&cur)[RL], BwdIn (&nxt)[RL]) {
+    load(t - 1, nxt);   // previous (earlier) step's inputs, in flight under this step
+    const int pb = t & 1;
+    int pa[RL];
+    float pv[RL], pd[RL], cz[RL];
+#pragma unroll
+    for (int ii = 0; ii < RL; ++ii) {
+      const int i = 4 * ii + q;
       pa[ii] = -1;
-      pv[ii] = pd[ii] = 0.0f;
+      pv[ii] = pd[ii] = cz[ii] = 0.0f;
       if (i >= RW) continue;
-      float dh = carry[ii], gr = 0, gz = 0, gn = 0, ghn = 0, hp = 0, x1 = 0;
-      if (r < R) {
-        const int64_t tr = (int64_t)t * R + r;
-        if (t < d.T) {
-          const int b = (int)fdiv((uint32_t)r, d.dN), ag = r - b * d.n;
-          const float dchv = w.dch[(int64_t)t * R + r];
-          const int a = (int)rp.actions[(rp.ep(b) * d.t_stride + t) * d.n + ag];
-          dh += dchv * W2[a * H + k];
-          pa[ii] = a;
-          pv[ii] = dchv * ht[ii];   // dW2[a][k] += dchosen * h_t[k]
-          pd[ii] = dchv;
-        }
-        const float* g = w.Gates + tr * (4 * H);
-        gr = g[k]; gz = g[H + k]; gn = g[2 * H + k]; ghn = g[3 * H + k];
-        hp = t > 0 ? w.Hs[(tr - R) * H + k] : 0.0f;
-        x1 = w.X1[tr * H + k];
+      const bool live = rv[ii];
+      const float gr = live ? cur[ii].gr : 0.0f, gz = live ? cur[ii].gz : 0.0f;
+      const float gn = live ? cur[ii].gn : 0.0f, ghn = live ? cur[ii].ghn : 0.0f;
+      const float hp = (live && t > 0) ? cur[ii].hp : 0.0f, x1 = live ? cur[ii].x1 : 0.0f;
+      float dh = carry[ii];
+      if (live && t < T) {
+        const float dchv = cur[ii].dch;
+        const int a = cur[ii].act;
+        dh += dchv * w2_s[a * H + k];
+        pa[ii] = a;
+        pv[ii] = dchv * ht[ii];   // dW2[a][k] += dchosen * h_t[k]
+        pd[ii] = dchv;
       }
       const float dn = dh * (1.0f - gz);
       const float dz = dh * (hp - gn);
       const float dan = dn * (1.0f - gn * gn);
       const float dar = (dan * ghn) * (gr * (1.0f - gr));
       const float daz = dz * (gz * (1.0f - gz));
-      if (r < R) {
-        float* o = w.dGI + ((int64_t)t * R + r) * G3;
+      if (live) {
+        float* o = w.dGI + ((int64_t)t * R + rr[ii]) * G3;
         o[k] = dar; o[H + k] = daz; o[2 * H + k] = dan;
       }
       dgi_s[pb][i][k] = dar; dgi_s[pb][i][H + k] = daz; dgi_s[pb][i][2 * H + k] = dan;
@@ -250,23 +293,35 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(Dims d, Rep rp, const floa
       const f32x4* dg4 = (const f32x4*)(&dgh_s[pb][i][48 * q]);
       const f32x4* di4 = (const f32x4*)(&dgi_s[pb][i][48 * q]);
       const float hpk = hp_s[pb][i][k], x1k = x1_s[pb][i][k];
-      float a0 = 0.0f, a1 = 0.0f;
+      float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
 #pragma unroll
       for (int c4 = 0; c4 < 12; ++c4) {
         const f32x4 dg = dg4[c4], di = di4[c4];
+        const int c = 4 * c4;
+        a0 = fmaf(wT[c], dg[0], a0); a1 = fmaf(wT[c + 1], dg[1], a1);
+        a2 = fmaf(wT[c + 2], dg[2], a2); a3 = fmaf(wT[c + 3], dg[3], a3);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int c = 4 * c4 + e;
-          if (e & 1) a1 = fmaf(wT[c], dg[e], a1); else a0 = fmaf(wT[c], dg[e], a0);
-          accH[c] = fmaf(dg[e], hpk, accH[c]);
-          accI[c] = fmaf(di[e], x1k, accI[c]);
+          accH[c + e] = fmaf(dg[e], hpk, accH[c + e]);
+          accI[c + e] = fmaf(di[e], x1k, accI[c + e]);
         }
       }
-      s[i] = quad_sum(a0 + a1);
+      s[i] = quad_sum((a0 + a1) + (a2 + a3));
     }
 #pragma unroll
     for (int ii = 0; ii < RL; ++ii) carry[ii] = cz[ii] + pick_row<RW>(s, ii, q);
+  };
+
+  BwdIn sa[RL], sb[RL];
+  load(d.Tp - 1, sa);
+  drain_vmem();
+  lds_barrier();
+  int t = d.Tp - 1;
+  for (; t - 1 >= 0; t -= 2) {
+    step(t, sa, sb);
+    step(t - 1, sb, sa);
   }
+  if (t >= 0) step(t, sa, sb);
 
   // per-workgroup partial slab
   float* slab = w.slab_rnn + (int64_t)blockIdx.x * slab_len;

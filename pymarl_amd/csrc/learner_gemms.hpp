@@ -5,6 +5,7 @@
 //             (BasicMAC._build_inputs one-hot columns folded into the epilogue as column gathers,
 //              basic_controller.py:100-135; fc1 + relu of rnn_agent.py:32)
 //   GiProb  : GI = X1 W_ih^T + b_ih                 (GRUCell input gates)
+//   Fc2Prob : Q = Hs W2^T + b2                      (fc2 over the recurrence's stored hidden states)
 //   HypProb : HYP = state_row W_hyper^T + b_hyper   (QMixer hyper_w_1 | hyper_w_final | hyper_b_1 | V.0,
 //             qmix.py:30-39; online on state[:, :-1], target on state[:, 1:])
 // Backward:
@@ -133,6 +134,55 @@ struct GiProb {
     for (int reg = 0; reg < 16; ++reg) {
       const int m = m0 + wm * 32 + acc_row(reg, lane);
       if (m < M) out[(int64_t)m * G3 + j] = acc[reg] + bj;
+    }
+  }
+  MQ_DEV void rowsum_out(int, int, float) const {}
+};
+
+// Q = Hs W2^T + b2 for both nets (fc2 of rnn_agent.py:35, out of the recurrence).
+struct Fc2Prob {
+  const float* Hs;   // [2][M][H]
+  const float* P0;
+  const float* P1;
+  int64_t o_w, o_b;
+  float* Q;          // [2][M][A]
+  int64_t M;
+  int A;
+  using APat = KPat;
+  using BPat = KPat;
+  static constexpr bool kRowSum = false;
+  struct Ctx {
+    const float* arow;
+    const float* brow;
+  };
+  MQ_DEV Ctx make_ctx(int m0, int n0, int z, int tid) const {
+    Ctx c;
+    const int m = m0 + KPat::row(tid);
+    c.arow = (m < M) ? Hs + ((int64_t)z * M + m) * H : nullptr;
+    const int nn = n0 + KPat::row(tid);
+    c.brow = (nn < A) ? (z ? P1 : P0) + o_w + (int64_t)nn * H : nullptr;
+    return c;
+  }
+  MQ_DEV void krange(int, int& kb, int& ke) const { kb = 0; ke = H; }
+  MQ_DEV void load_a(const Ctx& c, int k0, int, float (&r)[4]) const {
+    const int k = k0 + KPat::kq(threadIdx.x);
+    f32x4 v = c.arow ? *(const f32x4*)(c.arow + k) : f32x4{0, 0, 0, 0};
+    r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; r[3] = v[3];
+  }
+  MQ_DEV void load_b(const Ctx& c, int k0, int, float (&r)[4]) const {
+    const int k = k0 + KPat::kq(threadIdx.x);
+    f32x4 v = c.brow ? *(const f32x4*)(c.brow + k) : f32x4{0, 0, 0, 0};
+    r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; r[3] = v[3];
+  }
+  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int m0, int n0, int z, int wm, int wn, int lane) const {
+    const int j = n0 + wn * 32 + (lane & 31);
+    if (j >= A) return;
+    const float bj = (z ? P1 : P0)[o_b + j];
+    float* out = Q + (int64_t)z * M * A;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int m = m0 + wm * 32 + acc_row(reg, lane);
+      if (m < M) out[(int64_t)m * A + j] = acc[reg] + bj;
     }
   }
   MQ_DEV void rowsum_out(int, int, float) const {}

@@ -39,7 +39,7 @@ struct Lay {
 struct Work {
   float* X1;      // [2][RT][H]   relu(fc1) per net
   float* GI;      // [2][RT][3H]  W_ih x1 + b_ih per net
-  float* Hs;      // [RT][H]      online hidden after step t
+  float* Hs;      // [2][RT][H]   hidden after step t per net
   float* Gates;   // [RT][4H]     online r, z, n, W_hn h + b_hn
   float* Q;       // [2][RT][A]   mac_out / target_mac_out
   float* HYP;     // [2][M][NH]   QMIX hypernet outputs per net (state t for online, t+1 for target)

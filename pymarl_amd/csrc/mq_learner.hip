@@ -3,7 +3,8 @@
 // One train step (QLearner.train, q_learner.py:37-116) is this stream-ordered launch sequence:
 //   fc1      gemm  X1 = relu(W1 [obs | a_{t-1} | id] + b1)               both nets, rows gathered by episode id
 //   gi       gemm  GI = W_ih X1 + b_ih                                    both nets
-//   gru_fwd  recur h_t = GRU(GI_t, h_{t-1}); q_t = W2 h_t + b2           both nets, serial over T
+//   gru_fwd  recur h_t = GRU(GI_t, h_{t-1})                              both nets, serial over T
+//   fc2      gemm  Q = W2 H + b2                                          both nets
 //   hyper    gemm  QMIX hypernet outputs of state[:, :-1] / state[:, 1:] both nets (QMIX only)
 //   mix      per (t, episode): chosen gather, double-Q select, mixer fwd, TD, masked L2 sums, mixer bwd
 //   gru_bwd  recur BPTT; dW_hh, dW_ih, dW2 and biases accumulated in-kernel, dGI written out
@@ -48,9 +49,9 @@ int set_err(int code, const std::string& msg) {
 
 constexpr int kNsplitMax = 128;
 constexpr int kNormBlocks = 256;
-enum Phase { PH_FC1, PH_GI, PH_GRUF, PH_HYP, PH_MIX, PH_GRUB, PH_DX1, PH_DW1, PH_DWH, PH_RED, PH_NORM,
+enum Phase { PH_FC1, PH_GI, PH_GRUF, PH_FC2, PH_HYP, PH_MIX, PH_GRUB, PH_DX1, PH_DW1, PH_DWH, PH_RED, PH_NORM,
              PH_APPLY, PH_N };
-const char* kPhaseNames = "fc1;gi;gru_fwd;hyper;mix;gru_bwd;dx1;dw1;dwh;reduce;norm;apply";
+const char* kPhaseNames = "fc1;gi;gru_fwd;fc2;hyper;mix;gru_bwd;dx1;dw1;dwh;reduce;norm;apply";
 
 int pick_rw(int R, int max_blocks) {
   const int rws[4] = {1, 2, 4, 8};
@@ -185,7 +186,7 @@ template <int RW>
 hipError_t launch_gru_bwd(const Dims& d, const Rep& rp, const mq_handle* h, const Lay& L, const Work& w,
                           hipStream_t s, int* nblk) {
   *nblk = (d.R + RW - 1) / RW;
-  const size_t dyn = ((size_t)d.A * mq::H + d.A) * sizeof(float);
+  const size_t dyn = ((size_t)2 * d.A * mq::H + d.A) * sizeof(float);
   hipLaunchKernelGGL(gru_bwd_kernel<RW>, dim3(*nblk), dim3(256), dyn, s, d, rp, (const float*)h->on, L, w,
                      h->len_rnn);
   return hipGetLastError();
@@ -252,7 +253,7 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
   int64_t sizes[18] = {
       2 * RT * Hd,                                   // X1
       2 * RT * 3 * Hd,                               // GI
-      RT * Hd,                                       // Hs
+      2 * RT * Hd,                                   // Hs (both nets)
       RT * 4 * Hd,                                   // Gates
       2 * RT * A,                                    // Q
       2 * Mm * NH,                                   // HYP
@@ -348,6 +349,11 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
                  : rw == 4 ? launch_gru_fwd<4>(d, h, L, w, s)
                            : launch_gru_fwd<8>(d, h, L, w, s);
     MQ_HIP(e);
+  }
+  pt.begin(PH_FC2);
+  {
+    Fc2Prob p{w.Hs, h->on, h->tg, h->off[MQ_P_FC2_W], h->off[MQ_P_FC2_B], w.Q, RT, d.A};
+    MQ_HIP(launch_gemm(p, (int)RT, d.A, 2, s));
   }
   if (c.mixer == MQ_MIXER_QMIX) {
     pt.begin(PH_HYP);

@@ -44,19 +44,44 @@ int main(int argc, char** argv) {
   float* P1 = dev_rand(o, 0.12f);
   Work w{};
   w.GI = dev_rand(2 * RT * 192, 1.0f);
-  CK(hipMalloc(&w.Hs, RT * 64 * 4)); CK(hipMalloc(&w.Gates, RT * 256 * 4)); CK(hipMalloc(&w.Q, 2 * RT * A * 4));
+  CK(hipMalloc(&w.Hs, 2 * RT * 64 * 4)); CK(hipMalloc(&w.Gates, RT * 256 * 4)); CK(hipMalloc(&w.Q, 2 * RT * A * 4));
   auto run = [&](auto kern, int rw) {
     dim3 grid((d.R + rw - 1) / rw, 2);
     return time_it([&] { hipLaunchKernelGGL(kern, grid, dim3(256), 0, 0, d, (const float*)P0, (const float*)P1, L, w); });
   };
   printf("B=%d n=%d T=%d rows=%d\n", B, n, T, d.R);
-  printf("fwd RW1 V0 %.1f us\n", run(gru_fwd_kernel<1, 0>, 1));
+  printf("fwd RW1 %.1f us\n", run(gru_fwd_kernel<1, 0>, 1));
   printf("fwd RW1 V1(no Hs/Gates st) %.1f us\n", run(gru_fwd_kernel<1, 1>, 1));
-  printf("fwd RW1 V2(no fc2) %.1f us\n", run(gru_fwd_kernel<1, 2>, 1));
-  printf("fwd RW1 V3(no st, no fc2) %.1f us\n", run(gru_fwd_kernel<1, 3>, 1));
-  printf("fwd RW1 V4(no prefetch) %.1f us\n", run(gru_fwd_kernel<1, 4>, 1));
-  printf("fwd RW1 V7(none) %.1f us\n", run(gru_fwd_kernel<1, 7>, 1));
-  printf("fwd RW2 V0 %.1f us\n", run(gru_fwd_kernel<2, 0>, 2));
-  printf("fwd RW4 V0 %.1f us\n", run(gru_fwd_kernel<4, 0>, 4));
+  {
+    CK(hipMalloc(&w.slab_mix, 2 * 8 * 2 * d.R));
+    run(gru_fwd_kernel<1, 2>, 1);
+    std::vector<uint64_t> st(2 * 2 * d.R);
+    CK(hipMemcpy(st.data(), w.slab_mix, st.size() * 8, hipMemcpyDeviceToHost));
+    double cyc = 0, tick = 0;
+    for (int i = 0; i < 2 * d.R; ++i) { cyc += st[2 * i]; tick += st[2 * i + 1]; }
+    cyc /= 2 * d.R; tick /= 2 * d.R;
+    printf("fwd RW1 stamped: %.0f cycles/step, %.3f us/step, clock %.2f GHz\n", cyc / d.Tp, tick / 100.0 / d.Tp,
+           cyc / (tick * 10.0));
+  }
+  printf("fwd RW2 %.1f us\n", run(gru_fwd_kernel<2, 0>, 2));
+  printf("fwd RW4 %.1f us\n", run(gru_fwd_kernel<4, 0>, 4));
+  printf("fwd RW8 %.1f us\n", run(gru_fwd_kernel<8, 0>, 8));
+  // backward
+  CK(hipMalloc(&w.X1, RT * 64 * 4)); CK(hipMemset(w.X1, 0, RT * 64 * 4));
+  w.dch = dev_rand(RT, 0.1f);
+  CK(hipMalloc(&w.dGI, RT * 192 * 4));
+  int64_t len_rnn = L.o[MQ_P_FC2_B] + A - L.o[MQ_P_RNN_W_IH];
+  CK(hipMalloc(&w.slab_rnn, (int64_t)d.R * len_rnn * 4));
+  std::vector<int64_t> acts((int64_t)B * (T + 1) * n);
+  for (auto& a : acts) a = rand() % A;
+  int64_t* dacts; CK(hipMalloc(&dacts, acts.size() * 8)); CK(hipMemcpy(dacts, acts.data(), acts.size() * 8, hipMemcpyHostToDevice));
+  Rep rp{}; rp.actions = dacts;
+  auto runb = [&](auto kern, int rw) {
+    size_t dyn = (2 * A * 64 + A) * 4;
+    return time_it([&] { hipLaunchKernelGGL(kern, dim3((d.R + rw - 1) / rw), dim3(256), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn); });
+  };
+  printf("bwd RW1 %.1f us\n", runb(gru_bwd_kernel<1, 0>, 1));
+  printf("bwd RW2 %.1f us\n", runb(gru_bwd_kernel<2, 0>, 2));
+  printf("bwd RW4 %.1f us\n", runb(gru_bwd_kernel<4, 0>, 4));
   return 0;
 }
