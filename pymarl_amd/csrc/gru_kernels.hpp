@@ -51,7 +51,7 @@ template <int RW, bool ONLINE, int VAR>
 MQ_DEV void gru_fwd_body(const Dims& d, const float* __restrict__ P, const Lay& L, const Work& w, int z) {
   constexpr int RL = (RW + 3) / 4;
   const int tid = threadIdx.x, j = tid >> 2, q = tid & 3;
-  const int R = d.R, A = d.A, Tp = d.Tp;
+  const int R = d.R, Tp = d.Tp;
   const int64_t RT = d.RT();
   __shared__ float hbuf[2][RW][H];
 
@@ -167,38 +167,48 @@ __global__ __launch_bounds__(256) void gru_fwd_kernel(Dims d, const float* __res
 }
 
 // ------------------------------------------------------------------------------------------------ backward
-// BPTT over the online net (q_learner.py:100-101). grid = ceil(R / RW). Writes dGI for the dX1 GEMM and a
-// per-workgroup partial slab [w_ih | w_hh | b_ih | b_hh | fc2.w | fc2.b] of the gradient.
+// BPTT over the online net (q_learner.py:100-101). grid = ceil(R / RW), 512 threads = two wave roles:
+//  * chain waves (0-3, s_setprio 2): the serial part — gate derivatives from dh, the W_hh^T mat-vec, the carry;
+//  * accumulator waves (4-7): dW_hh += dgh h_{t-1}^T, dW_ih += dgi x1^T and the fc2 grads for the same step,
+//    read from the same LDS buffers after the step barrier. Half the per-step FMAs leave the chain; on each SIMD the
+//    accumulator wave fills the chain wave's LDS / barrier / transcendental bubbles.
+// Writes dGI for the dX1 GEMM and a per-workgroup slab [w_ih | w_hh | b_ih | b_hh | fc2.w | fc2.b].
 struct BwdIn {
   float gr, gz, gn, ghn, hp, x1, dch;
   int act;
 };
 
 template <int RW, int VAR = 0>
-__global__ __launch_bounds__(256) void gru_bwd_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
+__global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
                                                       Work w, int64_t slab_len) {
   constexpr int RL = (RW + 3) / 4;
-  const int tid = threadIdx.x, k = tid >> 2, q = tid & 3;
+  const int tid = threadIdx.x;
+  const bool chain = tid < 256;
+  const int lt = tid & 255, k = lt >> 2, q = lt & 3;
   const int R = d.R, A = d.A, T = d.T;
   __shared__ float dgh_s[2][RW][G3];
   __shared__ float dgi_s[2][RW][G3];
   __shared__ float hp_s[2][RW][H];
   __shared__ float x1_s[2][RW][H];
+  __shared__ float dch_s[2][RW];   // per row: dLoss/dchosen (0 at t = T) and its action, for the fc2 grads
+  __shared__ int act_s[2][RW];
   extern __shared__ float dyn[];   // W2 [A][H] | dW2 partial [A][H] | db2 [A]
   float* w2_s = dyn;
   float* dw2_s = dyn + A * H;
   float* db2_s = dyn + 2 * A * H;
 
+  // Role-shared registers (the roles are disjoint per thread, so one allocation serves both):
+  //   chain waves: wT = W_hh[48q..48q+47][k] (accI unused); accumulator waves: wT = dW_hh, accI = dW_ih slices.
+  float wT[48], accI[48];
   const float* Whh = P + L.o[MQ_P_RNN_W_HH];
-  float wT[48], accH[48], accI[48];
 #pragma unroll
   for (int c = 0; c < 48; ++c) {
-    wT[c] = Whh[(48 * q + c) * H + k];
-    accH[c] = 0.0f;
+    wT[c] = chain ? Whh[(48 * q + c) * H + k] : 0.0f;
     accI[c] = 0.0f;
   }
-  for (int i = tid; i < A * H; i += 256) { w2_s[i] = P[L.o[MQ_P_FC2_W] + i]; dw2_s[i] = 0.0f; }
-  for (int i = tid; i < A; i += 256) db2_s[i] = 0.0f;
+  float (&accH)[48] = wT;
+  for (int i = tid; i < A * H; i += 512) { w2_s[i] = P[L.o[MQ_P_FC2_W] + i]; dw2_s[i] = 0.0f; }
+  for (int i = tid; i < A; i += 512) db2_s[i] = 0.0f;
 
   const int r0 = blockIdx.x * RW;
   int rr[RL];
@@ -227,35 +237,28 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(Dims d, Rep rp, const floa
     }
   };
 
-  float carry[RL], ht[RL];
+  float carry[RL];
   float dbi0 = 0, dbi1 = 0, dbi2 = 0, dbh2 = 0;
 #pragma unroll
-  for (int ii = 0; ii < RL; ++ii) { carry[ii] = 0.0f; ht[ii] = 0.0f; }
+  for (int ii = 0; ii < RL; ++ii) carry[ii] = 0.0f;
 
-  auto step = [&](int t, const BwdIn (&cur)[RL], BwdIn (&nxt)[RL]) {
+  auto chain_pre = [&](int t, const BwdIn (&cur)[RL], BwdIn (&nxt)[RL], float (&cz)[RL]) {
     load(t - 1, nxt);   // previous (earlier) step's inputs, in flight under this step
     const int pb = t & 1;
-    int pa[RL];
-    float pv[RL], pd[RL], cz[RL];
 #pragma unroll
     for (int ii = 0; ii < RL; ++ii) {
       const int i = 4 * ii + q;
-      pa[ii] = -1;
-      pv[ii] = pd[ii] = cz[ii] = 0.0f;
+      cz[ii] = 0.0f;
       if (i >= RW) continue;
       const bool live = rv[ii];
       const float gr = live ? cur[ii].gr : 0.0f, gz = live ? cur[ii].gz : 0.0f;
       const float gn = live ? cur[ii].gn : 0.0f, ghn = live ? cur[ii].ghn : 0.0f;
       const float hp = (live && t > 0) ? cur[ii].hp : 0.0f, x1 = live ? cur[ii].x1 : 0.0f;
       float dh = carry[ii];
-      if (live && t < T) {
-        const float dchv = cur[ii].dch;
-        const int a = cur[ii].act;
-        dh += dchv * w2_s[a * H + k];
-        pa[ii] = a;
-        pv[ii] = dchv * ht[ii];   // dW2[a][k] += dchosen * h_t[k]
-        pd[ii] = dchv;
-      }
+      const float dchv = (live && t < T) ? cur[ii].dch : 0.0f;
+      const int a = cur[ii].act;
+      dh += dchv * w2_s[a * H + k];
+      if (k == 0) { dch_s[pb][i] = dchv; act_s[pb][i] = a; }
       const float dn = dh * (1.0f - gz);
       const float dz = dh * (hp - gn);
       const float dan = dn * (1.0f - gn * gn);
@@ -271,49 +274,69 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(Dims d, Rep rp, const floa
       x1_s[pb][i][k] = x1;
       dbi0 += dar; dbi1 += daz; dbi2 += dan; dbh2 += dan * gr;
       cz[ii] = dh * gz;
-      ht[ii] = hp;   // h_{t-1} is the next (earlier) step's h_t
     }
-    // fc2 gradient into LDS; the four lanes of a quad share unit k and may share an action, so they take
-    // turns (separate instructions) instead of racing on the same word.
-#pragma unroll
-    for (int ii = 0; ii < RL; ++ii) {
-#pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) {
-        if (q == s2 && pa[ii] >= 0) {
-          dw2_s[pa[ii] * H + k] += pv[ii];
-          if (k == 0) db2_s[pa[ii]] += pd[ii];
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
-    lds_barrier();
+  };
+  auto chain_post = [&](int t, const float (&cz)[RL]) {
+    const int pb = t & 1;
     float s[RW];
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
       const f32x4* dg4 = (const f32x4*)(&dgh_s[pb][i][48 * q]);
-      const f32x4* di4 = (const f32x4*)(&dgi_s[pb][i][48 * q]);
-      const float hpk = hp_s[pb][i][k], x1k = x1_s[pb][i][k];
       float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
 #pragma unroll
       for (int c4 = 0; c4 < 12; ++c4) {
-        const f32x4 dg = dg4[c4], di = di4[c4];
+        const f32x4 dg = dg4[c4];
         const int c = 4 * c4;
         a0 = fmaf(wT[c], dg[0], a0); a1 = fmaf(wT[c + 1], dg[1], a1);
         a2 = fmaf(wT[c + 2], dg[2], a2); a3 = fmaf(wT[c + 3], dg[3], a3);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          accH[c + e] = fmaf(dg[e], hpk, accH[c + e]);
-          accI[c + e] = fmaf(di[e], x1k, accI[c + e]);
-        }
       }
       s[i] = quad_sum((a0 + a1) + (a2 + a3));
     }
 #pragma unroll
     for (int ii = 0; ii < RL; ++ii) carry[ii] = cz[ii] + pick_row<RW>(s, ii, q);
   };
+  auto accumulate = [&](int t) {
+    const int pb = t & 1;
+    // fc2 grads: dW2[a][k] += dchosen * h_t[k]; (a, k) is owned by lane (k, q = a % 4), so no two lanes ever
+    // update the same word. h_t is the hp_s of step t+1 (still intact: that buffer is rewritten at step t-1).
+    if (t < T) {
+#pragma unroll
+      for (int i = 0; i < RW; ++i) {
+        const int a = act_s[pb][i];
+        if ((a & 3) == q) {
+          const float dchv = dch_s[pb][i];
+          dw2_s[a * H + k] += dchv * hp_s[pb ^ 1][i][k];
+          if (k == 0) db2_s[a] += dchv;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+      const f32x4* dg4 = (const f32x4*)(&dgh_s[pb][i][48 * q]);
+      const f32x4* di4 = (const f32x4*)(&dgi_s[pb][i][48 * q]);
+      const float hpk = hp_s[pb][i][k], x1k = x1_s[pb][i][k];
+#pragma unroll
+      for (int c4 = 0; c4 < 12; ++c4) {
+        const f32x4 dg = dg4[c4], di = di4[c4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          accH[4 * c4 + e] = fmaf(dg[e], hpk, accH[4 * c4 + e]);
+          accI[4 * c4 + e] = fmaf(di[e], x1k, accI[4 * c4 + e]);
+        }
+      }
+    }
+  };
+  auto step = [&](int t, const BwdIn (&cur)[RL], BwdIn (&nxt)[RL]) {
+    float cz[RL];
+    if (chain) chain_pre(t, cur, nxt, cz);
+    lds_barrier();
+    if (chain) chain_post(t, cz);
+    else accumulate(t);
+  };
 
+  if (chain) __builtin_amdgcn_s_setprio(2);
   BwdIn sa[RL], sb[RL];
-  load(d.Tp - 1, sa);
+  if (chain) load(d.Tp - 1, sa);
   drain_vmem();
   lds_barrier();
   int t = d.Tp - 1;
@@ -322,25 +345,29 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(Dims d, Rep rp, const floa
     step(t - 1, sb, sa);
   }
   if (t >= 0) step(t, sa, sb);
+  __builtin_amdgcn_s_setprio(0);
 
   // per-workgroup partial slab
   float* slab = w.slab_rnn + (int64_t)blockIdx.x * slab_len;
   const int64_t base = L.o[MQ_P_RNN_W_IH];
   const int64_t o_ih = 0, o_hh = L.o[MQ_P_RNN_W_HH] - base, o_bi = L.o[MQ_P_RNN_B_IH] - base,
                 o_bh = L.o[MQ_P_RNN_B_HH] - base, o_w2 = L.o[MQ_P_FC2_W] - base, o_b2 = L.o[MQ_P_FC2_B] - base;
+  if (!chain) {
 #pragma unroll
-  for (int c = 0; c < 48; ++c) {
-    slab[o_ih + (48 * q + c) * H + k] = accI[c];
-    slab[o_hh + (48 * q + c) * H + k] = accH[c];
-  }
-  dbi0 = quad_sum(dbi0); dbi1 = quad_sum(dbi1); dbi2 = quad_sum(dbi2); dbh2 = quad_sum(dbh2);
-  if (q == 0) {
-    slab[o_bi + k] = dbi0; slab[o_bi + H + k] = dbi1; slab[o_bi + 2 * H + k] = dbi2;
-    slab[o_bh + k] = dbi0; slab[o_bh + H + k] = dbi1; slab[o_bh + 2 * H + k] = dbh2;
+    for (int c = 0; c < 48; ++c) {
+      slab[o_ih + (48 * q + c) * H + k] = accI[c];
+      slab[o_hh + (48 * q + c) * H + k] = accH[c];
+    }
+  } else {
+    dbi0 = quad_sum(dbi0); dbi1 = quad_sum(dbi1); dbi2 = quad_sum(dbi2); dbh2 = quad_sum(dbh2);
+    if (q == 0) {
+      slab[o_bi + k] = dbi0; slab[o_bi + H + k] = dbi1; slab[o_bi + 2 * H + k] = dbi2;
+      slab[o_bh + k] = dbi0; slab[o_bh + H + k] = dbi1; slab[o_bh + 2 * H + k] = dbh2;
+    }
   }
   lds_barrier();
-  for (int i = tid; i < A * H; i += 256) slab[o_w2 + i] = dw2_s[i];
-  for (int i = tid; i < A; i += 256) slab[o_b2 + i] = db2_s[i];
+  for (int i = tid; i < A * H; i += 512) slab[o_w2 + i] = dw2_s[i];
+  for (int i = tid; i < A; i += 512) slab[o_b2 + i] = db2_s[i];
 }
 
 }  // namespace mq

@@ -1,17 +1,18 @@
 // The learner's row-parallel and weight-gradient contractions as policies of gemm_f32_kernel.
 //
 // Forward (grid.z = net: 0 online, 1 target; both nets read the same replay rows):
-//   Fc1Prob : X1 = relu(obs_row . W1[:, :O]^T + W1[:, O + a_{t-1}] + W1[:, O + A + agent] + b1)
-//             (BasicMAC._build_inputs one-hot columns folded into the epilogue as column gathers,
-//              basic_controller.py:100-135; fc1 + relu of rnn_agent.py:32)
+//   Fc1Prob : X1 = relu(xin W1^T + b1), xin = [obs_t | onehot(a_{t-1}) | onehot(agent)] built on the fly from the
+//             replay rows gathered by episode id (BasicMAC._build_inputs, basic_controller.py:100-135; fc1 + relu,
+//             rnn_agent.py:32); the online pass also writes xin densely (XIN) for the dW1 contraction
 //   GiProb  : GI = X1 W_ih^T + b_ih                 (GRUCell input gates)
 //   Fc2Prob : Q = Hs W2^T + b2                      (fc2 over the recurrence's stored hidden states)
 //   HypProb : HYP = state_row W_hyper^T + b_hyper   (QMixer hyper_w_1 | hyper_w_final | hyper_b_1 | V.0,
-//             qmix.py:30-39; online on state[:, :-1], target on state[:, 1:])
+//             qmix.py:30-39; online on state[:, :-1], target on state[:, 1:]); the online pass writes the
+//             gathered states densely (S0) for the dW_hyper contraction
 // Backward:
 //   Dx1Prob : dP1 = (dGI W_ih) * [X1 > 0]
-//   Dw1Prob : [dW1 | db1] = dP1^T [xin]   split-K over (t, row); one-hot columns generated on the fly
-//   DwhProb : [dW_hyper | db_hyper] = dHYP^T [state]   split-K over (t, episode)
+//   Dw1Prob : [dW1 | db1] = dP1^T XIN                  split-K over (t, row)
+//   DwhProb : [dW_hyper | db_hyper] = dHYP^T S0        split-K over (t, episode)
 #pragma once
 #include "gemm_f32.hpp"
 #include "learner_types.hpp"
@@ -25,14 +26,29 @@ MQ_DEV void krange_split(int K, int nsplit, int z, int& kb, int& ke) {
   ke = min(K, kb + chunk);
 }
 
+MQ_DEV void ld4(const float* p, float (&r)[4]) {   // 16-B aligned row segment, or zeros
+  f32x4 v = p ? *(const f32x4*)p : f32x4{0, 0, 0, 0};
+  r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; r[3] = v[3];
+}
+
+// C tile store helper: rows mrow0 + acc_row(reg), column ncol0 + lane%32.
+template <class F>
+MQ_DEV void for_tile(const f32x16& acc, int mrow0, int ncol0, int lane, F&& f) {
+  const int j = ncol0 + (lane & 31);
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) f(mrow0 + acc_row(reg, lane), j, acc[reg]);
+}
+
 // ---------------------------------------------------------------------------------------------- forward
 struct Fc1Prob {
+  static constexpr int BN = 64;
   Dims d;
   Rep rp;
   const float* P0;
   const float* P1;
   int64_t o_w, o_b;
-  float* X1;
+  float* X1;   // [2][M][H]
+  float* XIN;  // [M][I], written by the z == 0 pass
   int64_t M;
   using APat = KPat;
   using BPat = KPat;
@@ -40,59 +56,66 @@ struct Fc1Prob {
   struct Ctx {
     const float* arow;
     const float* brow;
+    int m, aprev, ag;
   };
   MQ_DEV Ctx make_ctx(int m0, int n0, int z, int tid) const {
     Ctx c;
-    const int m = m0 + KPat::row(tid);
+    c.m = m0 + KPat::row(tid);
     c.arow = nullptr;
-    if (m < M) {
+    c.aprev = -1;
+    c.ag = -1;
+    if (c.m < M) {
       int t, r, b, ag;
-      split_tr(d, (uint32_t)m, t, r, b, ag);
-      c.arow = rp.obs + ((rp.ep(b) * d.t_stride + t) * d.n + ag) * (int64_t)d.O;
+      split_tr(d, (uint32_t)c.m, t, r, b, ag);
+      const int64_t slot = rp.ep(b) * d.t_stride + t;
+      c.arow = rp.obs + (slot * d.n + ag) * (int64_t)d.O;
+      c.ag = ag;
+      // actions_onehot[t-1] is zero unless slot t-1 was filled (runner contract, synthetic.py)
+      if (d.last_action && t > 0 && rp.filled[slot - 1]) c.aprev = (int)rp.actions[(slot - 1) * d.n + ag];
     }
     const int nn = n0 + KPat::row(tid);
     c.brow = (nn < H) ? (z ? P1 : P0) + o_w + (int64_t)nn * d.I : nullptr;
     return c;
   }
-  MQ_DEV void krange(int, int& kb, int& ke) const { kb = 0; ke = d.O; }
+  MQ_DEV void krange(int, int& kb, int& ke) const { kb = 0; ke = d.I; }
+  MQ_DEV float xin(const Ctx& c, int k) const {
+    if (k < d.O) return c.arow[k];
+    int f = k - d.O;
+    if (d.last_action) {
+      if (f < d.A) return f == c.aprev ? 1.0f : 0.0f;
+      f -= d.A;
+    }
+    return f == c.ag ? 1.0f : 0.0f;
+  }
   MQ_DEV void load_a(const Ctx& c, int k0, int ke, float (&r)[4]) const {
     const int k = k0 + KPat::kq(threadIdx.x);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = (c.arow && k + i < ke) ? c.arow[k + i] : 0.0f;
+    for (int i = 0; i < 4; ++i) r[i] = (c.arow && k + i < ke) ? xin(c, k + i) : 0.0f;
+    if (XIN && c.arow && blockIdx.z == 0 && blockIdx.y == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (k + i < ke) XIN[(int64_t)c.m * d.I + k + i] = r[i];
+    }
   }
-  MQ_DEV void load_b(const Ctx& c, int k0, int ke, float (&r)[4]) const {
+  MQ_DEV void load_b(const Ctx& c, int, int k0, int ke, float (&r)[4]) const {
     const int k = k0 + KPat::kq(threadIdx.x);
 #pragma unroll
     for (int i = 0; i < 4; ++i) r[i] = (c.brow && k + i < ke) ? c.brow[k + i] : 0.0f;
   }
-  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int m0, int n0, int z, int wm, int wn, int lane) const {
-    const float* P = z ? P1 : P0;
-    const float* W = P + o_w;
-    const int j = n0 + wn * 32 + (lane & 31);
+  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int z, int lane) const {
+    const int j = ncol0 + (lane & 31);
     if (j >= H) return;
-    const float bj = P[o_b + j];
-    const int a_off = d.O, id_off = d.O + (d.last_action ? d.A : 0);
+    const float bj = (z ? P1 : P0)[o_b + j];
     float* out = X1 + (int64_t)z * M * H;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int m = m0 + wm * 32 + acc_row(reg, lane);
-      if (m >= M) continue;
-      int t, r, b, ag;
-      split_tr(d, (uint32_t)m, t, r, b, ag);
-      float v = acc[reg] + bj;
-      if (d.last_action && t > 0) {
-        const int64_t e = rp.ep(b);
-        const int64_t slot = e * d.t_stride + (t - 1);
-        if (rp.filled[slot]) v += W[(int64_t)j * d.I + a_off + (int)rp.actions[slot * d.n + ag]];
-      }
-      if (d.agent_id) v += W[(int64_t)j * d.I + id_off + ag];
-      out[(int64_t)m * H + j] = fmaxf(v, 0.0f);
-    }
+    for_tile(acc, mrow0, ncol0, lane, [&](int m, int jj, float v) {
+      if (m < M) out[(int64_t)m * H + jj] = fmaxf(v + bj, 0.0f);
+    });
   }
   MQ_DEV void rowsum_out(int, int, float) const {}
 };
 
 struct GiProb {
+  static constexpr int BN = 192;
   const float* X1;   // [2][M][H]
   const float* P0;
   const float* P1;
@@ -104,43 +127,38 @@ struct GiProb {
   static constexpr bool kRowSum = false;
   struct Ctx {
     const float* arow;
-    const float* brow;
+    const float* brow[3];
   };
-  MQ_DEV Ctx make_ctx(int m0, int n0, int z, int tid) const {
+  MQ_DEV Ctx make_ctx(int m0, int, int z, int tid) const {
     Ctx c;
     const int m = m0 + KPat::row(tid);
     c.arow = (m < M) ? X1 + ((int64_t)z * M + m) * H : nullptr;
-    const int nn = n0 + KPat::row(tid);
-    c.brow = (nn < G3) ? (z ? P1 : P0) + o_w + (int64_t)nn * H : nullptr;
+    const float* W = (z ? P1 : P0) + o_w;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) c.brow[p] = W + (int64_t)(64 * p + KPat::row(tid)) * H;
     return c;
   }
   MQ_DEV void krange(int, int& kb, int& ke) const { kb = 0; ke = H; }
   MQ_DEV void load_a(const Ctx& c, int k0, int, float (&r)[4]) const {
-    const int k = k0 + KPat::kq(threadIdx.x);
-    f32x4 v = c.arow ? *(const f32x4*)(c.arow + k) : f32x4{0, 0, 0, 0};
-    r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; r[3] = v[3];
+    ld4(c.arow ? c.arow + k0 + KPat::kq(threadIdx.x) : nullptr, r);
   }
-  MQ_DEV void load_b(const Ctx& c, int k0, int, float (&r)[4]) const {
-    const int k = k0 + KPat::kq(threadIdx.x);
-    f32x4 v = c.brow ? *(const f32x4*)(c.brow + k) : f32x4{0, 0, 0, 0};
-    r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; r[3] = v[3];
+  MQ_DEV void load_b(const Ctx& c, int pass, int k0, int, float (&r)[4]) const {
+    ld4(c.brow[pass] + k0 + KPat::kq(threadIdx.x), r);
   }
-  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int m0, int n0, int z, int wm, int wn, int lane) const {
-    const int j = n0 + wn * 32 + (lane & 31);
-    if (j >= G3) return;
+  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int z, int lane) const {
+    const int j = ncol0 + (lane & 31);
     const float bj = (z ? P1 : P0)[o_b + j];
     float* out = GI + (int64_t)z * M * G3;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int m = m0 + wm * 32 + acc_row(reg, lane);
-      if (m < M) out[(int64_t)m * G3 + j] = acc[reg] + bj;
-    }
+    for_tile(acc, mrow0, ncol0, lane, [&](int m, int jj, float v) {
+      if (m < M) out[(int64_t)m * G3 + jj] = v + bj;
+    });
   }
   MQ_DEV void rowsum_out(int, int, float) const {}
 };
 
 // Q = Hs W2^T + b2 for both nets (fc2 of rnn_agent.py:35, out of the recurrence).
 struct Fc2Prob {
+  static constexpr int BN = 64;
   const float* Hs;   // [2][M][H]
   const float* P0;
   const float* P1;
@@ -165,25 +183,19 @@ struct Fc2Prob {
   }
   MQ_DEV void krange(int, int& kb, int& ke) const { kb = 0; ke = H; }
   MQ_DEV void load_a(const Ctx& c, int k0, int, float (&r)[4]) const {
-    const int k = k0 + KPat::kq(threadIdx.x);
-    f32x4 v = c.arow ? *(const f32x4*)(c.arow + k) : f32x4{0, 0, 0, 0};
-    r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; r[3] = v[3];
+    ld4(c.arow ? c.arow + k0 + KPat::kq(threadIdx.x) : nullptr, r);
   }
-  MQ_DEV void load_b(const Ctx& c, int k0, int, float (&r)[4]) const {
-    const int k = k0 + KPat::kq(threadIdx.x);
-    f32x4 v = c.brow ? *(const f32x4*)(c.brow + k) : f32x4{0, 0, 0, 0};
-    r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; r[3] = v[3];
+  MQ_DEV void load_b(const Ctx& c, int, int k0, int, float (&r)[4]) const {
+    ld4(c.brow ? c.brow + k0 + KPat::kq(threadIdx.x) : nullptr, r);
   }
-  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int m0, int n0, int z, int wm, int wn, int lane) const {
-    const int j = n0 + wn * 32 + (lane & 31);
+  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int z, int lane) const {
+    const int j = ncol0 + (lane & 31);
     if (j >= A) return;
     const float bj = (z ? P1 : P0)[o_b + j];
     float* out = Q + (int64_t)z * M * A;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int m = m0 + wm * 32 + acc_row(reg, lane);
-      if (m < M) out[(int64_t)m * A + j] = acc[reg] + bj;
-    }
+    for_tile(acc, mrow0, ncol0, lane, [&](int m, int jj, float v) {
+      if (m < M) out[(int64_t)m * A + jj] = v + bj;
+    });
   }
   MQ_DEV void rowsum_out(int, int, float) const {}
 };
@@ -203,32 +215,38 @@ MQ_DEV HypSeg hyp_seg(const Lay& L, int nE, int E, int j) {
 }
 
 struct HypProb {
+  static constexpr int BN = 192;
   Dims d;
   Rep rp;
   Lay L;
   const float* P0;
   const float* P1;
   float* HYP;   // [2][M][NH]
+  float* S0;    // [M][S] gathered state[:, :-1] rows, written by the z == 0 pass
   using APat = KPat;
   using BPat = KPat;
   static constexpr bool kRowSum = false;
   struct Ctx {
     const float* arow;
-    const float* brow;
+    const float* brow[3];
+    int m;
   };
   MQ_DEV Ctx make_ctx(int m0, int n0, int z, int tid) const {
     Ctx c;
-    const int m = m0 + KPat::row(tid);
+    c.m = m0 + KPat::row(tid);
     c.arow = nullptr;
-    if (m < d.M) {
-      const int t = (int)fdiv((uint32_t)m, d.dB), b = m - t * d.B;
+    if (c.m < d.M) {
+      const int t = (int)fdiv((uint32_t)c.m, d.dB), b = c.m - t * d.B;
       c.arow = rp.state + (rp.ep(b) * d.t_stride + t + z) * (int64_t)d.S;
     }
-    const int nn = n0 + KPat::row(tid);
-    c.brow = nullptr;
-    if (nn < d.NH) {
-      HypSeg s = hyp_seg(L, d.n * d.E, d.E, nn);
-      c.brow = (z ? P1 : P0) + s.w + (int64_t)s.row * d.S;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int nn = n0 + 64 * p + KPat::row(tid);
+      c.brow[p] = nullptr;
+      if (nn < d.NH) {
+        HypSeg s = hyp_seg(L, d.n * d.E, d.E, nn);
+        c.brow[p] = (z ? P1 : P0) + s.w + (int64_t)s.row * d.S;
+      }
     }
     return c;
   }
@@ -237,29 +255,34 @@ struct HypProb {
     const int k = k0 + KPat::kq(threadIdx.x);
 #pragma unroll
     for (int i = 0; i < 4; ++i) r[i] = (c.arow && k + i < ke) ? c.arow[k + i] : 0.0f;
-  }
-  MQ_DEV void load_b(const Ctx& c, int k0, int ke, float (&r)[4]) const {
-    const int k = k0 + KPat::kq(threadIdx.x);
+    if (S0 && c.arow && blockIdx.z == 0 && blockIdx.y == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = (c.brow && k + i < ke) ? c.brow[k + i] : 0.0f;
+      for (int i = 0; i < 4; ++i)
+        if (k + i < ke) S0[(int64_t)c.m * d.S + k + i] = r[i];
+    }
   }
-  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int m0, int n0, int z, int wm, int wn, int lane) const {
-    const int j = n0 + wn * 32 + (lane & 31);
+  MQ_DEV void load_b(const Ctx& c, int pass, int k0, int ke, float (&r)[4]) const {
+    const int k = k0 + KPat::kq(threadIdx.x);
+    const float* p = c.brow[pass];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = (p && k + i < ke) ? p[k + i] : 0.0f;
+  }
+  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int z, int lane) const {
+    const int j = ncol0 + (lane & 31);
     if (j >= d.NH) return;
     HypSeg s = hyp_seg(L, d.n * d.E, d.E, j);
     const float bj = (z ? P1 : P0)[s.b + s.row];
     float* out = HYP + (int64_t)z * d.M * d.NH;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int m = m0 + wm * 32 + acc_row(reg, lane);
-      if (m < d.M) out[(int64_t)m * d.NH + j] = acc[reg] + bj;
-    }
+    for_tile(acc, mrow0, ncol0, lane, [&](int m, int jj, float v) {
+      if (m < d.M) out[(int64_t)m * d.NH + jj] = v + bj;
+    });
   }
   MQ_DEV void rowsum_out(int, int, float) const {}
 };
 
 // ---------------------------------------------------------------------------------------------- backward
 struct Dx1Prob {
+  static constexpr int BN = 64;
   const float* dGI;   // [M][3H]
   const float* Wih;   // online w_ih [3H][H]
   const float* X1o;   // online X1 [M][H]
@@ -279,34 +302,30 @@ struct Dx1Prob {
   }
   MQ_DEV void krange(int, int& kb, int& ke) const { kb = 0; ke = G3; }
   MQ_DEV void load_a(const Ctx& c, int k0, int, float (&r)[4]) const {
-    const int k = k0 + KPat::kq(threadIdx.x);
-    f32x4 v = c.arow ? *(const f32x4*)(c.arow + k) : f32x4{0, 0, 0, 0};
-    r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; r[3] = v[3];
+    ld4(c.arow ? c.arow + k0 + KPat::kq(threadIdx.x) : nullptr, r);
   }
-  MQ_DEV void load_b(const Ctx&, int k0, int, float (&r)[4]) const {
+  MQ_DEV void load_b(const Ctx&, int, int k0, int, float (&r)[4]) const {
     const int nn = MPat::row(threadIdx.x), k = k0 + MPat::kq(threadIdx.x);
 #pragma unroll
     for (int i = 0; i < 4; ++i) r[i] = Wih[(int64_t)(k + i) * H + nn];
   }
-  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int m0, int n0, int, int wm, int wn, int lane) const {
-    const int j = n0 + wn * 32 + (lane & 31);
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int m = m0 + wm * 32 + acc_row(reg, lane);
+  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int, int lane) const {
+    for_tile(acc, mrow0, ncol0, lane, [&](int m, int j, float v) {
       if (m < M) {
         const int64_t o = (int64_t)m * H + j;
-        dP1[o] = X1o[o] > 0.0f ? acc[reg] : 0.0f;
+        dP1[o] = X1o[o] > 0.0f ? v : 0.0f;
       }
-    }
+    });
   }
   MQ_DEV void rowsum_out(int, int, float) const {}
 };
 
 // [dW1 | db1] slab: out row j (hidden unit), out col f (agent input feature), reduction over rows tr.
 struct Dw1Prob {
-  Dims d;
-  Rep rp;
+  static constexpr int BN = 128;
+  int I;
   const float* dP1;   // [RT][H]
+  const float* XIN;   // [RT][I]
   float* slab;        // [nsplit][H*I + H]
   int64_t K;          // RT
   int nsplit;
@@ -314,56 +333,40 @@ struct Dw1Prob {
   using BPat = MPat;
   static constexpr bool kRowSum = true;
   struct Ctx {
-    int f;
+    int f0;
   };
   MQ_DEV Ctx make_ctx(int, int n0, int, int tid) const { return Ctx{n0 + MPat::row(tid)}; }
   MQ_DEV void krange(int z, int& kb, int& ke) const { krange_split((int)K, nsplit, z, kb, ke); }
   MQ_DEV void load_a(const Ctx&, int k0, int ke, float (&r)[4]) const {
-    const int j = blockIdx.x * GBM + MPat::row(threadIdx.x), k = k0 + MPat::kq(threadIdx.x);
+    const int j = MPat::row(threadIdx.x), k = k0 + MPat::kq(threadIdx.x);
 #pragma unroll
     for (int i = 0; i < 4; ++i) r[i] = (k + i < ke) ? dP1[(int64_t)(k + i) * H + j] : 0.0f;
   }
-  MQ_DEV float xin(uint32_t tr, int f) const {
-    int t, r, b, ag;
-    split_tr(d, tr, t, r, b, ag);
-    const int64_t slot = rp.ep(b) * d.t_stride + t;
-    if (f < d.O) return rp.obs[(slot * d.n + ag) * d.O + f];
-    f -= d.O;
-    if (d.last_action) {
-      if (f < d.A) {
-        if (t == 0 || !rp.filled[slot - 1]) return 0.0f;
-        return (int)rp.actions[(slot - 1) * d.n + ag] == f ? 1.0f : 0.0f;
-      }
-      f -= d.A;
-    }
-    return (d.agent_id && f == ag) ? 1.0f : 0.0f;
-  }
-  MQ_DEV void load_b(const Ctx& c, int k0, int ke, float (&r)[4]) const {
-    const int k = k0 + MPat::kq(threadIdx.x);
+  MQ_DEV void load_b(const Ctx& c, int pass, int k0, int ke, float (&r)[4]) const {
+    const int f = c.f0 + 64 * pass, k = k0 + MPat::kq(threadIdx.x);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = (c.f < d.I && k + i < ke) ? xin((uint32_t)(k + i), c.f) : 0.0f;
+    for (int i = 0; i < 4; ++i) r[i] = (f < I && k + i < ke) ? XIN[(int64_t)(k + i) * I + f] : 0.0f;
   }
-  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int m0, int n0, int z, int wm, int wn, int lane) const {
-    const int f = n0 + wn * 32 + (lane & 31);
-    if (f >= d.I) return;
-    float* out = slab + (int64_t)z * (H * d.I + H);
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int j = m0 + wm * 32 + acc_row(reg, lane);
-      if (j < H) out[(int64_t)j * d.I + f] = acc[reg];
-    }
+  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int z, int lane) const {
+    const int f = ncol0 + (lane & 31);
+    if (f >= I) return;
+    float* out = slab + (int64_t)z * (H * I + H);
+    for_tile(acc, mrow0, ncol0, lane, [&](int j, int ff, float v) {
+      if (j < H) out[(int64_t)j * I + ff] = v;
+    });
   }
   MQ_DEV void rowsum_out(int j, int z, float v) const {
-    if (j < H) slab[(int64_t)z * (H * d.I + H) + H * d.I + j] = v;
+    if (j < H) slab[(int64_t)z * (H * I + H) + H * I + j] = v;
   }
 };
 
 // [dW_hyper | db_hyper] slab over the contiguous QMixer region hyper_w_1.weight .. V.0.bias.
 struct DwhProb {
+  static constexpr int BN = 192;
   Dims d;
-  Rep rp;
   Lay L;
   const float* dHYP;   // [M][NH]
+  const float* S0;     // [M][S]
   float* slab;         // [nsplit][len]
   int64_t len;
   int nsplit;
@@ -371,7 +374,7 @@ struct DwhProb {
   using BPat = MPat;
   static constexpr bool kRowSum = true;
   struct Ctx {
-    int s;
+    int s0;
   };
   MQ_DEV Ctx make_ctx(int, int n0, int, int tid) const { return Ctx{n0 + MPat::row(tid)}; }
   MQ_DEV void krange(int z, int& kb, int& ke) const { krange_split(d.M, nsplit, z, kb, ke); }
@@ -380,31 +383,22 @@ struct DwhProb {
 #pragma unroll
     for (int i = 0; i < 4; ++i) r[i] = (j < d.NH && k + i < ke) ? dHYP[(int64_t)(k + i) * d.NH + j] : 0.0f;
   }
-  MQ_DEV void load_b(const Ctx& c, int k0, int ke, float (&r)[4]) const {
-    const int k = k0 + MPat::kq(threadIdx.x);
+  MQ_DEV void load_b(const Ctx& c, int pass, int k0, int ke, float (&r)[4]) const {
+    const int s = c.s0 + 64 * pass, k = k0 + MPat::kq(threadIdx.x);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float v = 0.0f;
-      if (c.s < d.S && k + i < ke) {
-        const int m = k + i, t = (int)fdiv((uint32_t)m, d.dB), b = m - t * d.B;
-        v = rp.state[(rp.ep(b) * d.t_stride + t) * (int64_t)d.S + c.s];
-      }
-      r[i] = v;
-    }
+    for (int i = 0; i < 4; ++i) r[i] = (s < d.S && k + i < ke) ? S0[(int64_t)(k + i) * d.S + s] : 0.0f;
   }
-  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int m0, int n0, int z, int wm, int wn, int lane) const {
-    const int s = n0 + wn * 32 + (lane & 31);
+  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int z, int lane) const {
+    const int s = ncol0 + (lane & 31);
     if (s >= d.S) return;
     float* out = slab + (int64_t)z * len;
     const int64_t base = L.o[MQ_P_HW1_W];
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int j = m0 + wm * 32 + acc_row(reg, lane);
+    for_tile(acc, mrow0, ncol0, lane, [&](int j, int ss, float v) {
       if (j < d.NH) {
         HypSeg sg = hyp_seg(L, d.n * d.E, d.E, j);
-        out[sg.w - base + (int64_t)sg.row * d.S + s] = acc[reg];
+        out[sg.w - base + (int64_t)sg.row * d.S + ss] = v;
       }
-    }
+    });
   }
   MQ_DEV void rowsum_out(int j, int z, float v) const {
     if (j < d.NH) {

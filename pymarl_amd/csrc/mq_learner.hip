@@ -187,7 +187,7 @@ hipError_t launch_gru_bwd(const Dims& d, const Rep& rp, const mq_handle* h, cons
                           hipStream_t s, int* nblk) {
   *nblk = (d.R + RW - 1) / RW;
   const size_t dyn = ((size_t)2 * d.A * mq::H + d.A) * sizeof(float);
-  hipLaunchKernelGGL(gru_bwd_kernel<RW>, dim3(*nblk), dim3(256), dyn, s, d, rp, (const float*)h->on, L, w,
+  hipLaunchKernelGGL(gru_bwd_kernel<RW>, dim3(*nblk), dim3(512), dyn, s, d, rp, (const float*)h->on, L, w,
                      h->len_rnn);
   return hipGetLastError();
 }
@@ -250,7 +250,7 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
                                     (int64_t)((kNsplitMax + kRedZ - 1) / kRedZ) * h->len_mix,
                                     ((nmix + kRedZ - 1) / kRedZ) * (h->E + 1),
                                     ((nmix + kRedZ - 1) / kRedZ) * 8});
-  int64_t sizes[18] = {
+  int64_t sizes[20] = {
       2 * RT * Hd,                                   // X1
       2 * RT * 3 * Hd,                               // GI
       2 * RT * Hd,                                   // Hs (both nets)
@@ -269,9 +269,11 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
       kNormBlocks,                                   // norm_part
       Mm * n,                                        // curmax (int32)
       red_tmp,                                       // two-pass reduction partials
+      RT * h->I,                                     // XIN (dense agent inputs)
+      Mm * c.state_dim,                              // S0 (gathered state[:, :-1] rows)
   };
-  int64_t total = 0, offs[18];
-  for (int i = 0; i < 18; ++i) { offs[i] = total; total += align_up(std::max<int64_t>(sizes[i], 1)); }
+  int64_t total = 0, offs[20];
+  for (int i = 0; i < 20; ++i) { offs[i] = total; total += align_up(std::max<int64_t>(sizes[i], 1)); }
   hipError_t e = hipMalloc(&h->ws, total * sizeof(float));
   if (e != hipSuccess) {
     delete h;
@@ -287,6 +289,8 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
   w.norm_part = base + offs[15];
   h->curmax_ws = (int32_t*)(base + offs[16]);
   w.red_tmp = base + offs[17];
+  w.XIN = base + offs[18];
+  w.S0 = base + offs[19];
   w.curmax = h->curmax_ws;
   *out = h;
   return MQ_OK;
@@ -333,7 +337,7 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
 
   pt.begin(PH_FC1);
   {
-    Fc1Prob p{d, rp, h->on, h->tg, h->off[MQ_P_FC1_W], h->off[MQ_P_FC1_B], w.X1, RT};
+    Fc1Prob p{d, rp, h->on, h->tg, h->off[MQ_P_FC1_W], h->off[MQ_P_FC1_B], w.X1, w.XIN, RT};
     MQ_HIP(launch_gemm(p, (int)RT, mq::H, 2, s));
   }
   pt.begin(PH_GI);
@@ -357,7 +361,7 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   }
   if (c.mixer == MQ_MIXER_QMIX) {
     pt.begin(PH_HYP);
-    HypProb p{d, rp, L, h->on, h->tg, w.HYP};
+    HypProb p{d, rp, L, h->on, h->tg, w.HYP, w.S0};
     MQ_HIP(launch_gemm(p, d.M, d.NH, 2, s));
   }
   pt.begin(PH_MIX);
@@ -367,8 +371,8 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   MQ_HIP(hipGetLastError());
   pt.begin(PH_GRUB);
   {
-    // RW = 8 would spill the 144 live accumulator/weight registers per lane; cap at 4
-    const int rw = std::min(4, pick_rw(d.R, 256));
+    // RW >= 4 spills the 96 role registers + per-row prefetch sets at 512 threads; cap at 2
+    const int rw = std::min(2, pick_rw(d.R, 256));
     hipError_t e = rw == 1 ? launch_gru_bwd<1>(d, rp, h, L, w, s, &h->nblk_bwd)
                  : rw == 2 ? launch_gru_bwd<2>(d, rp, h, L, w, s, &h->nblk_bwd)
                            : launch_gru_bwd<4>(d, rp, h, L, w, s, &h->nblk_bwd);
@@ -381,24 +385,24 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   }
   pt.begin(PH_DW1);
   {
-    const int tiles = (d.I + GBN - 1) / GBN;
+    const int tiles = (d.I + Dw1Prob::BN - 1) / Dw1Prob::BN;
     int ns = (int)std::min<int64_t>(kNsplitMax, std::max<int64_t>(1, RT / 256));
     ns = std::max(1, std::min(ns, (512 + tiles - 1) / tiles));
     // keep every split non-empty under krange_split's GBK rounding
     int64_t chunk = ((RT + ns - 1) / ns + GBK - 1) / GBK * GBK;
     ns = (int)((RT + chunk - 1) / chunk);
     h->nsplit_fc1 = ns;
-    Dw1Prob p{d, rp, w.dP1, w.slab_fc1, RT, ns};
+    Dw1Prob p{d.I, w.dP1, w.XIN, w.slab_fc1, RT, ns};
     MQ_HIP(launch_gemm(p, mq::H, d.I, ns, s));
   }
   if (c.mixer == MQ_MIXER_QMIX) {
     pt.begin(PH_DWH);
-    const int tiles = ((d.NH + GBM - 1) / GBM) * ((d.S + GBN - 1) / GBN);
+    const int tiles = ((d.NH + GBM - 1) / GBM) * ((d.S + DwhProb::BN - 1) / DwhProb::BN);
     int ns = std::max(1, std::min(kNsplitMax, std::min((512 + tiles - 1) / tiles, d.M / 64)));
     int64_t chunk = ((d.M + ns - 1) / ns + GBK - 1) / GBK * GBK;
     ns = (int)((d.M + chunk - 1) / chunk);
     h->nsplit_mix = ns;
-    DwhProb p{d, rp, L, w.dHYP, w.slab_mix, h->len_mix, ns};
+    DwhProb p{d, L, w.dHYP, w.S0, w.slab_mix, h->len_mix, ns};
     MQ_HIP(launch_gemm(p, d.NH, d.S, ns, s));
   }
   pt.begin(PH_RED);
