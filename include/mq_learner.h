@@ -87,6 +87,9 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream);
 /* Normalise by sum(m), clip_grad_norm_(grad_norm_clip), RMSprop(lr, alpha, eps) step, write stats. */
 int mq_apply(mq_handle* h, void* stream);
 int mq_train_step(mq_handle* h, const mq_replay* batch, void* stream);
+/* Declare that the caller sums the gradient buffer across ranks between mq_forward_backward and mq_apply
+ * (mq_apply then recomputes the global gradient norm from the reduced buffer). */
+int mq_set_data_parallel(mq_handle* h, int32_t on);
 int mq_update_targets(mq_handle* h, void* stream);
 
 /* Copy an intermediate of the last mq_forward_backward into dst (device): 0 = online mac_out [t][b*n+a][A],

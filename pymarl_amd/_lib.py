@@ -25,7 +25,7 @@ P_COUNT = len(PARAM_NAMES)
 EXPORTS = [
     "mq_last_error", "mq_create", "mq_destroy", "mq_param_offsets", "mq_bind", "mq_forward_backward", "mq_apply",
     "mq_train_step", "mq_update_targets", "mq_copy_intermediate", "mq_mac_forward", "mq_agent_forward",
-    "mq_greedy_actions", "mq_set_timing", "mq_phase_times", "mq_phase_names",
+    "mq_greedy_actions", "mq_set_timing", "mq_phase_times", "mq_phase_names", "mq_set_data_parallel",
 ]
 
 
@@ -84,6 +84,7 @@ def load(required=True):
         "mq_agent_forward": ([vp, vp, i32, vp, vp, vp, i32, vp], ctypes.c_int),
         "mq_greedy_actions": ([vp, vp, vp, i32, i32, vp], ctypes.c_int),
         "mq_set_timing": ([vp, i32, ctypes.c_uint32], ctypes.c_int),
+        "mq_set_data_parallel": ([vp, i32], ctypes.c_int),
         "mq_phase_times": ([vp, ctypes.POINTER(ctypes.c_float), i32, ctypes.POINTER(i32)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():

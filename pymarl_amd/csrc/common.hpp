@@ -41,6 +41,11 @@ MQ_DEV float quad_xor1(float v) {
 MQ_DEV float quad_xor2(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
 }
+// Broadcast lane L of each quad to the whole quad.
+template <int L>
+MQ_DEV float quad_bcast(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), L * 0x55, 0xF, 0xF, true));
+}
 // Sum over the 4 lanes of a quad; every lane of the quad receives the same total ((a+b)+(c+d) order).
 MQ_DEV float quad_sum(float v) {
   v = v + quad_xor1(v);

@@ -73,8 +73,8 @@ MQ_DEV void gru_fwd_body(const Dims& d, const float* __restrict__ P, const Lay& 
   bool rv[RL];
 #pragma unroll
   for (int ii = 0; ii < RL; ++ii) {
-    const int i = 4 * ii + q, r = r0 + i;
-    rv[ii] = i < RW && r < R;
+    const int i = RW == 1 ? 0 : 4 * ii + q, r = r0 + i;   // RW == 1: all four lanes of a quad share the row
+    rv[ii] = (RW == 1 || i < RW) && r < R;
     rr[ii] = min(r, R - 1);
   }
   for (int i = tid; i < RW * H; i += 256) hbuf[0][i / H][i % H] = 0.0f;   // init_hidden: h0 = 0
@@ -83,10 +83,14 @@ MQ_DEV void gru_fwd_body(const Dims& d, const float* __restrict__ P, const Lay& 
   float* Hz = w.Hs + (int64_t)z * RT * H;
   auto load = [&](int t, float (&g)[RL][3]) {
     const int tc = min(t, Tp - 1);
+    if constexpr (RW == 1) {   // lane-split gates: lane q of the quad owns gate component min(q, 2)
+      g[0][0] = GI[((int64_t)tc * R + rr[0]) * G3 + min(q, 2) * H + j];
+    } else {
 #pragma unroll
-    for (int ii = 0; ii < RL; ++ii) {
-      const float* p = GI + ((int64_t)tc * R + rr[ii]) * G3;
-      g[ii][0] = p[j]; g[ii][1] = p[H + j]; g[ii][2] = p[2 * H + j];
+      for (int ii = 0; ii < RL; ++ii) {
+        const float* p = GI + ((int64_t)tc * R + rr[ii]) * G3;
+        g[ii][0] = p[j]; g[ii][1] = p[H + j]; g[ii][2] = p[2 * H + j];
+      }
     }
   };
   auto step = [&](int t, const float (&cur)[RL][3], float (&nxt)[RL][3]) {
@@ -112,6 +116,27 @@ MQ_DEV void gru_fwd_body(const Dims& d, const float* __restrict__ P, const Lay& 
       sr[i] = quad_sum(ar + ar2);
       sz[i] = quad_sum(az + az2);
       sn[i] = quad_sum(an + an2);
+    }
+    if constexpr (RW == 1) {
+      // One row, four lanes per unit: lane 0 computes r, lane 1 z (one sigmoid sequence for both), lane 2 n,
+      // broadcast inside the quad by DPP; lane q stores gate component q. 1/4 of the gate VALU of the
+      // one-lane form, and one GI load / one Gates store per lane.
+      const float own = cur[0][0];
+      const float gh = q == 0 ? sr[0] + bhr : (q == 1 ? sz[0] + bhz : 0.0f);
+      const float sg = sigm_fast(gh + own);
+      const float rg = quad_bcast<0>(sg), zg = quad_bcast<1>(sg);
+      const float ghn = sn[0] + bhn;
+      const float ng = quad_bcast<2>(tanh_fast(own + ghn * rg));
+      const float hp = hb[0][j];
+      const float h1 = (hp - ng) * zg + ng;   // ATen gru_cell: (hx - n) * z + n
+      if (q == 0) hn[0][j] = h1;
+      if (!(VAR & 1) && rv[0]) {
+        const int64_t tr = (int64_t)t * R + rr[0];
+        if (q == 0) Hz[tr * H + j] = h1;   // both nets: fc2 runs afterwards as a row-parallel GEMM over H
+        if (ONLINE) w.Gates[tr * (4 * H) + q * H + j] = q == 0 ? rg : (q == 1 ? zg : (q == 2 ? ng : ghn));
+      }
+      lds_barrier();
+      return;
     }
 #pragma unroll
     for (int ii = 0; ii < RL; ++ii) {

@@ -215,7 +215,7 @@ MQ_DEV HypSeg hyp_seg(const Lay& L, int nE, int E, int j) {
 }
 
 struct HypProb {
-  static constexpr int BN = 192;
+  static constexpr int BN = 64;   // M = T*B is small: more n-tiles keep more workgroups (and loads) in flight
   Dims d;
   Rep rp;
   Lay L;
@@ -228,7 +228,7 @@ struct HypProb {
   static constexpr bool kRowSum = false;
   struct Ctx {
     const float* arow;
-    const float* brow[3];
+    const float* brow[BN / 64];
     int m;
   };
   MQ_DEV Ctx make_ctx(int m0, int n0, int z, int tid) const {
@@ -240,7 +240,7 @@ struct HypProb {
       c.arow = rp.state + (rp.ep(b) * d.t_stride + t + z) * (int64_t)d.S;
     }
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
+    for (int p = 0; p < BN / 64; ++p) {
       const int nn = n0 + 64 * p + KPat::row(tid);
       c.brow[p] = nullptr;
       if (nn < d.NH) {

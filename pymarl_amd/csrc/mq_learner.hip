@@ -11,9 +11,8 @@
 //   dx1      gemm  dP1 = (dGI W_ih) * [X1 > 0]
 //   dw1      gemm  [dW1 | db1] = dP1^T xin                                split-K
 //   dwh      gemm  [dW_hyper | db_hyper] = dHYP^T state                   split-K (QMIX only)
-//   reduce   deterministic slab sums -> flat gradient buffer (+ loss sums)
+//   reduce   deterministic two-pass slab sums -> flat gradient buffer (+ loss sums), per-block sums of squares
 //   --- (data-parallel all-reduce of the gradient buffer happens here, in the caller)
-//   norm     partial sum of squares
 //   apply    / sum(mask), clip_grad_norm_, RMSprop
 #include <cstdio>
 #include <algorithm>
@@ -48,10 +47,9 @@ int set_err(int code, const std::string& msg) {
   } while (0)
 
 constexpr int kNsplitMax = 128;
-constexpr int kNormBlocks = 256;
-enum Phase { PH_FC1, PH_GI, PH_GRUF, PH_FC2, PH_HYP, PH_MIX, PH_GRUB, PH_DX1, PH_DW1, PH_DWH, PH_RED, PH_NORM,
-             PH_APPLY, PH_N };
-const char* kPhaseNames = "fc1;gi;gru_fwd;fc2;hyper;mix;gru_bwd;dx1;dw1;dwh;reduce;norm;apply";
+enum Phase { PH_FC1, PH_GI, PH_GRUF, PH_FC2, PH_HYP, PH_MIX, PH_GRUB, PH_DX1, PH_DW1, PH_DWH, PH_RED, PH_APPLY,
+             PH_N };
+const char* kPhaseNames = "fc1;gi;gru_fwd;fc2;hyper;mix;gru_bwd;dx1;dw1;dwh;reduce;apply";
 
 int pick_rw(int R, int max_blocks) {
   const int rws[4] = {1, 2, 4, 8};
@@ -78,7 +76,8 @@ struct mq_handle {
   // last step bookkeeping
   bool have_fb = false;
   Dims last;
-  int nsplit_fc1 = 1, nsplit_mix = 1, nblk_bwd = 1, nblk_mix = 1;
+  int nsplit_fc1 = 1, nsplit_mix = 1, nblk_bwd = 1, nblk_mix = 1, n_norm_part = 0;
+  bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
   int slots = 0;
   uint32_t mask = 0;
@@ -192,21 +191,25 @@ hipError_t launch_gru_bwd(const Dims& d, const Rep& rp, const mq_handle* h, cons
   return hipGetLastError();
 }
 
-int reduce_into(const float* slab, int nslab, int64_t len, float* dst, float* tmp, hipStream_t s) {
-  if (len <= 0) return MQ_OK;
-  const unsigned bx = (unsigned)((len + 255) / 256);
-  if (nslab <= 2 * kRedZ) {
-    hipLaunchKernelGGL(reduce_slabs_kernel, dim3(bx, 1), dim3(256), 0, s, slab, nslab, len, nslab, dst);
-    MQ_HIP(hipGetLastError());
-    return MQ_OK;
+// Plan the slab reductions of one step: regions in gradient order, then the loss sums (not part of the norm).
+struct RedBuilder {
+  RedPlan pl{};
+  int b1 = 0, b2 = 0;
+  float* tmp;
+  explicit RedBuilder(float* t) : tmp(t) {}
+  void add(const float* src, int nslab, int64_t len, float* dst, bool sq) {
+    if (len <= 0 || nslab <= 0) return;
+    RedRegion& R = pl.r[pl.nr++];
+    R.src = src; R.dst = dst; R.len = len; R.nslab = nslab; R.sq = sq ? 1 : 0;
+    R.zc = kRedZ;
+    R.ng = (nslab + kRedZ - 1) / kRedZ;
+    R.tmp = tmp;
+    tmp += R.ng * len;
+    const int nb = (int)((len + 255) / 256);
+    R.blk1 = b1; b1 += nb * R.ng;
+    R.blk2 = b2; b2 += nb;
   }
-  const int nz = (nslab + kRedZ - 1) / kRedZ;
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(bx, nz), dim3(256), 0, s, slab, nslab, len, kRedZ, tmp);
-  MQ_HIP(hipGetLastError());
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(bx, 1), dim3(256), 0, s, (const float*)tmp, nz, len, nz, dst);
-  MQ_HIP(hipGetLastError());
-  return MQ_OK;
-}
+};
 
 }  // namespace
 
@@ -245,11 +248,11 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
   const int64_t Rm = (int64_t)c.max_batch * n;
   const int64_t nmix = (Mm + 3) / 4;
   const int64_t NH = h->NH;
-  const int64_t red_tmp = std::max({((Rm + kRedZ - 1) / kRedZ) * h->len_rnn,
-                                    (int64_t)((kNsplitMax + kRedZ - 1) / kRedZ) * (Hd * h->I + Hd),
-                                    (int64_t)((kNsplitMax + kRedZ - 1) / kRedZ) * h->len_mix,
-                                    ((nmix + kRedZ - 1) / kRedZ) * (h->E + 1),
-                                    ((nmix + kRedZ - 1) / kRedZ) * 8});
+  auto ng = [](int64_t ns) { return (ns + kRedZ - 1) / kRedZ; };
+  const int64_t red_tmp = ng(Rm) * h->len_rnn + ng(kNsplitMax) * (Hd * h->I + Hd) + ng(kNsplitMax) * h->len_mix +
+                          ng(nmix) * (h->E + 1) + ng(nmix) * 8;
+  const int64_t norm_parts = (Hd * h->I + Hd + 255) / 256 + (h->len_rnn + 255) / 256 + (h->len_mix + 255) / 256 +
+                             (h->E + 1 + 255) / 256 + 1 + 8;
   int64_t sizes[20] = {
       2 * RT * Hd,                                   // X1
       2 * RT * 3 * Hd,                               // GI
@@ -266,7 +269,7 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
       (int64_t)kNsplitMax * h->len_mix,              // slab_mix
       nmix * (h->E + 1),                             // slab_v2
       nmix * 8,                                      // loss_part
-      kNormBlocks,                                   // norm_part
+      std::max<int64_t>(norm_parts, 256),            // norm_part
       Mm * n,                                        // curmax (int32)
       red_tmp,                                       // two-pass reduction partials
       RT * h->I,                                     // XIN (dense agent inputs)
@@ -406,14 +409,21 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
     MQ_HIP(launch_gemm(p, d.NH, d.S, ns, s));
   }
   pt.begin(PH_RED);
-  if ((rc = reduce_into(w.slab_fc1, h->nsplit_fc1, (int64_t)mq::H * d.I + mq::H, h->grad + h->off[MQ_P_FC1_W], w.red_tmp, s)))
-    return rc;
-  if ((rc = reduce_into(w.slab_rnn, h->nblk_bwd, h->len_rnn, h->grad + h->off[MQ_P_RNN_W_IH], w.red_tmp, s))) return rc;
-  if (c.mixer == MQ_MIXER_QMIX) {
-    if ((rc = reduce_into(w.slab_mix, h->nsplit_mix, h->len_mix, h->grad + h->off[MQ_P_HW1_W], w.red_tmp, s))) return rc;
-    if ((rc = reduce_into(w.slab_v2, h->nblk_mix, d.E + 1, h->grad + h->off[MQ_P_V2_W], w.red_tmp, s))) return rc;
+  {
+    RedBuilder rb(w.red_tmp);
+    rb.add(w.slab_fc1, h->nsplit_fc1, (int64_t)mq::H * d.I + mq::H, h->grad + h->off[MQ_P_FC1_W], true);
+    rb.add(w.slab_rnn, h->nblk_bwd, h->len_rnn, h->grad + h->off[MQ_P_RNN_W_IH], true);
+    if (c.mixer == MQ_MIXER_QMIX) {
+      rb.add(w.slab_mix, h->nsplit_mix, h->len_mix, h->grad + h->off[MQ_P_HW1_W], true);
+      rb.add(w.slab_v2, h->nblk_mix, d.E + 1, h->grad + h->off[MQ_P_V2_W], true);
+    }
+    rb.add(w.loss_part, h->nblk_mix, MQ_NSUMS, h->grad + h->P, false);
+    hipLaunchKernelGGL(red_pass1_kernel, dim3(rb.b1), dim3(256), 0, s, rb.pl);
+    MQ_HIP(hipGetLastError());
+    hipLaunchKernelGGL(red_pass2_kernel, dim3(rb.b2), dim3(256), 0, s, rb.pl, w.norm_part);
+    MQ_HIP(hipGetLastError());
+    h->n_norm_part = rb.b2;
   }
-  if ((rc = reduce_into(w.loss_part, h->nblk_mix, MQ_NSUMS, h->grad + h->P, w.red_tmp, s))) return rc;
   pt.end();
   h->last = d;
   h->have_fb = true;
@@ -425,17 +435,26 @@ int mq_apply(mq_handle* h, void* stream) {
   if (!h->have_fb) return set_err(MQ_ERR_STATE, "mq_apply before mq_forward_backward");
   hipStream_t s = (hipStream_t)stream;
   PhaseTimer pt{h, s};
-  pt.begin(PH_NORM);
-  hipLaunchKernelGGL(sumsq_kernel, dim3(kNormBlocks), dim3(256), 0, s, (const float*)h->grad, h->P, h->w.norm_part);
-  MQ_HIP(hipGetLastError());
   pt.begin(PH_APPLY);
+  if (h->dp) {   // the gradient was all-reduced after the reduce pass: its norm partials are stale
+    h->n_norm_part = 256;
+    hipLaunchKernelGGL(sumsq_kernel, dim3(h->n_norm_part), dim3(256), 0, s, (const float*)h->grad, h->P,
+                       h->w.norm_part);
+    MQ_HIP(hipGetLastError());
+  }
   OptHP hp{h->cfg.lr, h->cfg.optim_alpha, h->cfg.optim_eps, h->cfg.grad_norm_clip, h->cfg.n_agents};
   int blocks = (int)std::min<int64_t>((h->P + 255) / 256, 1024);
   hipLaunchKernelGGL(apply_kernel, dim3(blocks), dim3(256), 0, s, h->on, h->grad, h->sq, h->P,
-                     (const float*)h->w.norm_part, kNormBlocks, hp, h->stats);
+                     (const float*)h->w.norm_part, h->n_norm_part, hp, h->stats);
   MQ_HIP(hipGetLastError());
   pt.end();
   ++h->tstep;
+  return MQ_OK;
+}
+
+int mq_set_data_parallel(mq_handle* h, int32_t on) {
+  if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
+  h->dp = on != 0;
   return MQ_OK;
 }
 

@@ -6,25 +6,69 @@
 
 namespace mq {
 
-// dst[blockIdx.y*len + i] = sum over z in [y*zc, min(nslab, (y+1)*zc)) of slab[z*len + i], z ascending.
-// With gridDim.y == 1 this is the whole reduction; larger slab counts go through two passes (zc = 16, then the
-// partials) so thousands of workgroups keep 16 independent loads each in flight. Fixed order: bitwise
-// reproducible.
+// Deterministic two-pass reduction of every gradient slab of a train step in two launches (a launch costs
+// ~4.5 us on this path whatever its size, so one launch per region was the bigger cost):
+//   pass 1: block (region, z-group, chunk) sums zc consecutive slabs of its 256 elements -> tmp[group][len]
+//   pass 2: block (region, chunk) sums the groups in order -> dst, and writes its partial sum of squares of the
+//           gradient elements (regions with sq = 1) for clip_grad_norm_ -> norm_part[block]
+// Fixed summation order throughout: bitwise reproducible.
 constexpr int kRedZ = 16;
-__global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restrict__ slab, int nslab, int64_t len,
-                                                           int zc, float* __restrict__ dst) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= len) return;
-  const int z0 = blockIdx.y * zc, z1 = min(nslab, z0 + zc);
+constexpr int kRedMaxRegions = 6;
+struct RedRegion {
+  const float* src;
+  float* dst;
+  float* tmp;
+  int64_t len;
+  int nslab, zc, ng, sq;
+  int blk1, blk2;   // first block of this region in pass 1 / pass 2
+};
+struct RedPlan {
+  RedRegion r[kRedMaxRegions];
+  int nr;
+};
+
+MQ_DEV int red_region(const RedPlan& pl, int b, bool pass2) {
+  int k = 0;
+#pragma unroll
+  for (int j = 1; j < kRedMaxRegions; ++j)
+    if (j < pl.nr && b >= (pass2 ? pl.r[j].blk2 : pl.r[j].blk1)) k = j;
+  return k;
+}
+
+__global__ __launch_bounds__(256) void red_pass1_kernel(RedPlan pl) {
+  const int k = red_region(pl, blockIdx.x, false);
+  const RedRegion& R = pl.r[k];
+  const int nb = (int)((R.len + 255) / 256), lb = blockIdx.x - R.blk1, g = lb / nb, chunk = lb - g * nb;
+  const int64_t i = (int64_t)chunk * 256 + threadIdx.x;
+  if (i >= R.len) return;
+  const int z0 = g * R.zc, z1 = min(R.nslab, z0 + R.zc);
   float v[kRedZ];
   float s = 0.0f;
   for (int zb = z0; zb < z1; zb += kRedZ) {
 #pragma unroll
-    for (int u = 0; u < kRedZ; ++u) v[u] = (zb + u < z1) ? slab[(int64_t)(zb + u) * len + i] : 0.0f;
+    for (int u = 0; u < kRedZ; ++u) v[u] = (zb + u < z1) ? R.src[(int64_t)(zb + u) * R.len + i] : 0.0f;
 #pragma unroll
     for (int u = 0; u < kRedZ; ++u) s += v[u];
   }
-  dst[(int64_t)blockIdx.y * len + i] = s;
+  R.tmp[(int64_t)g * R.len + i] = s;
+}
+
+__global__ __launch_bounds__(256) void red_pass2_kernel(RedPlan pl, float* __restrict__ norm_part) {
+  const int k = red_region(pl, blockIdx.x, true);
+  const RedRegion& R = pl.r[k];
+  const int64_t i = (int64_t)(blockIdx.x - R.blk2) * 256 + threadIdx.x;
+  float sq = 0.0f;
+  if (i < R.len) {
+    float v = 0.0f;
+    for (int g = 0; g < R.ng; ++g) v += R.tmp[(int64_t)g * R.len + i];
+    R.dst[i] = v;
+    if (R.sq) sq = v * v;
+  }
+  __shared__ float red[4];
+  sq = wave_sum(sq);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
+  __syncthreads();
+  if (threadIdx.x == 0) norm_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // Per-block partial sum of squares of the (unnormalised) gradient.

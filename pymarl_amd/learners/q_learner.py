@@ -179,6 +179,12 @@ class QLearner:
             o += n
         self._handle = None
 
+    def _dp_active(self):
+        if not self.dp:
+            return False
+        import torch.distributed as dist
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
     def _get_handle(self, batch):
         T = batch.max_seq_length if not isinstance(batch, SampledBatch) else batch.source.max_seq_length
         need_b = max(batch.batch_size, getattr(self.args, "batch_size", 1))
@@ -191,6 +197,8 @@ class QLearner:
             self._curmax = th.zeros(Tmax * need_b * self.args.n_agents, dtype=th.int32, device=self._online.device)
             _lib.check(h.lib.mq_bind(h.h, _lib.ptr(self._online), _lib.ptr(self._target), _lib.ptr(self._grad),
                                      _lib.ptr(self._sq), _lib.ptr(self._stats), _lib.ptr(self._curmax)))
+            if self._dp_active() or getattr(self, "force_dp_norm", False):
+                _lib.check(h.lib.mq_set_data_parallel(h.h, 1))
             if h.n_params != self.n_params:
                 raise _lib.MQError("parameter layout mismatch: library {} vs modules {}".format(h.n_params,
                                                                                               self.n_params))

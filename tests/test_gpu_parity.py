@@ -157,3 +157,20 @@ def test_teacher_forced_steps(cases, name, steps):
         g_or = np.concatenate([v.ravel() for v in o.last["grads"].values()])
         assert rel(flat_grads(learner), g_or) < 1e-4, (name, k)
         assert rel(flat_params(learner), o.flat("params")) < 1e-5, (name, k)
+
+
+def test_data_parallel_norm_path_single_rank(cases):
+    """The data-parallel apply path (norm recomputed after the all-reduce) on one rank equals the local path."""
+    from tests.gpu_helpers import build, flat_params, rel
+    case = get_case(cases, "tiny_qmix")
+    outs = []
+    for force in (False, True):
+        args, buf, mac, learner, logger = build(case)
+        learner.force_dp_norm = force
+        np.random.seed(case.sampler_seed)
+        for k in range(2):
+            batch = buf.sample(case.B)
+            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
+        outs.append((flat_params(learner), learner.last_stats()["grad_norm"]))
+    assert rel(outs[1][0], outs[0][0]) < 1e-6
+    assert abs(outs[1][1] - outs[0][1]) <= 1e-5 * abs(outs[0][1])
