@@ -201,8 +201,9 @@ struct RedBuilder {
     if (len <= 0 || nslab <= 0) return;
     RedRegion& R = pl.r[pl.nr++];
     R.src = src; R.dst = dst; R.len = len; R.nslab = nslab; R.sq = sq ? 1 : 0;
-    R.zc = kRedZ;
-    R.ng = (nslab + kRedZ - 1) / kRedZ;
+    // at most kRedZ groups, so pass 2 sums <= 16 partials per element with all loads in flight
+    R.zc = (nslab + kRedZ - 1) / kRedZ;
+    R.ng = (nslab + R.zc - 1) / R.zc;
     R.tmp = tmp;
     tmp += R.ng * len;
     const int nb = (int)((len + 255) / 256);
@@ -248,7 +249,7 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
   const int64_t Rm = (int64_t)c.max_batch * n;
   const int64_t nmix = (Mm + 3) / 4;
   const int64_t NH = h->NH;
-  auto ng = [](int64_t ns) { return (ns + kRedZ - 1) / kRedZ; };
+  auto ng = [](int64_t ns) { return std::min<int64_t>(ns, kRedZ); };
   const int64_t red_tmp = ng(Rm) * h->len_rnn + ng(kNsplitMax) * (Hd * h->I + Hd) + ng(kNsplitMax) * h->len_mix +
                           ng(nmix) * (h->E + 1) + ng(nmix) * 8;
   const int64_t norm_parts = (Hd * h->I + Hd + 255) / 256 + (h->len_rnn + 255) / 256 + (h->len_mix + 255) / 256 +

@@ -9,6 +9,7 @@ namespace mq {
 // Deterministic two-pass reduction of every gradient slab of a train step in two launches (a launch costs
 // ~4.5 us on this path whatever its size, so one launch per region was the bigger cost):
 //   pass 1: block (region, z-group, chunk) sums zc consecutive slabs of its 256 elements -> tmp[group][len]
+//           (zc chosen so there are at most 16 groups)
 //   pass 2: block (region, chunk) sums the groups in order -> dst, and writes its partial sum of squares of the
 //           gradient elements (regions with sq = 1) for clip_grad_norm_ -> norm_part[block]
 // Fixed summation order throughout: bitwise reproducible.
@@ -59,8 +60,12 @@ __global__ __launch_bounds__(256) void red_pass2_kernel(RedPlan pl, float* __res
   const int64_t i = (int64_t)(blockIdx.x - R.blk2) * 256 + threadIdx.x;
   float sq = 0.0f;
   if (i < R.len) {
+    float u[kRedZ];
+#pragma unroll
+    for (int g = 0; g < kRedZ; ++g) u[g] = g < R.ng ? R.tmp[(int64_t)g * R.len + i] : 0.0f;
     float v = 0.0f;
-    for (int g = 0; g < R.ng; ++g) v += R.tmp[(int64_t)g * R.len + i];
+#pragma unroll
+    for (int g = 0; g < kRedZ; ++g) v += u[g];
     R.dst[i] = v;
     if (R.sq) sq = v * v;
   }
