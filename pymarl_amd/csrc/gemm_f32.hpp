@@ -61,39 +61,47 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const P p) {
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[nt][i] = 0.0f;
-  float ra[4], rb[NT][4], rsum = 0.0f;
-  if (kb < ke) {
-    p.load_a(ctx, kb, ke, ra);
+  // Two register sets: the loads for K-step i+2 are issued right after step i's tiles are published, so each load
+  // has two K-steps of MFMAs to land (a 64-wide tile's single step is ~0.25 us of MFMA, below HBM latency).
+  float ra[2][4], rb[2][NT][4], rsum = 0.0f;
 #pragma unroll
-    for (int pp = 0; pp < NT; ++pp) p.load_b(ctx, pp, kb, ke, rb[pp]);
+  for (int s = 0; s < 2; ++s) {
+    if (kb + s * GBK < ke) {
+      p.load_a(ctx, kb + s * GBK, ke, ra[s]);
+#pragma unroll
+      for (int pp = 0; pp < NT; ++pp) p.load_b(ctx, pp, kb + s * GBK, ke, rb[s][pp]);
+    }
   }
-  int buf = 0;
-  for (int k0 = kb; k0 < ke; k0 += GBK) {
-    P::APat::template store<GLDA>(As[buf], ra, tid, 0);
+  for (int k00 = kb; k00 < ke; k00 += 2 * GBK) {
 #pragma unroll
-    for (int pp = 0; pp < NT; ++pp) P::BPat::template store<LDB>(Bs[buf], rb[pp], tid, pp);
-    __syncthreads();
-    if (k0 + GBK < ke) {
-      p.load_a(ctx, k0 + GBK, ke, ra);
+    for (int s = 0; s < 2; ++s) {
+      const int k0 = k00 + s * GBK;
+      if (k0 >= ke) break;
+      P::APat::template store<GLDA>(As[s], ra[s], tid, 0);
 #pragma unroll
-      for (int pp = 0; pp < NT; ++pp) p.load_b(ctx, pp, k0 + GBK, ke, rb[pp]);
-    }
-    const float* a = As[buf] + (lane >> 5) * GLDA + wm * 32 + (lane & 31);
-    const float* b = Bs[buf] + (lane >> 5) * LDB + wn * (BN / 2) + (lane & 31);
+      for (int pp = 0; pp < NT; ++pp) P::BPat::template store<LDB>(Bs[s], rb[s][pp], tid, pp);
+      lds_barrier();   // LDS only: the other register set's loads stay in flight
+      if (k0 + 2 * GBK < ke) {
+        p.load_a(ctx, k0 + 2 * GBK, ke, ra[s]);
 #pragma unroll
-    for (int kk = 0; kk < GBK; kk += 2) {
-      const float av = a[kk * GLDA];
+        for (int pp = 0; pp < NT; ++pp) p.load_b(ctx, pp, k0 + 2 * GBK, ke, rb[s][pp]);
+      }
+      const float* a = As[s] + (lane >> 5) * GLDA + wm * 32 + (lane & 31);
+      const float* b = Bs[s] + (lane >> 5) * LDB + wn * (BN / 2) + (lane & 31);
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b[kk * LDB + nt * 32], acc[nt], 0, 0, 0);
-    }
-    if (P::kRowSum) {
-      if (blockIdx.y == 0 && tid < GBM) {
+      for (int kk = 0; kk < GBK; kk += 2) {
+        const float av = a[kk * GLDA];
 #pragma unroll
-        for (int kk = 0; kk < GBK; ++kk) rsum += As[buf][kk * GLDA + tid];
+        for (int nt = 0; nt < NT; ++nt)
+          acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b[kk * LDB + nt * 32], acc[nt], 0, 0, 0);
+      }
+      if (P::kRowSum) {
+        if (blockIdx.y == 0 && tid < GBM) {
+#pragma unroll
+          for (int kk = 0; kk < GBK; ++kk) rsum += As[s][kk * GLDA + tid];
+        }
       }
     }
-    buf ^= 1;
   }
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) p.epilogue(ctx, acc[nt], m0 + wm * 32, n0 + wn * (BN / 2) + nt * 32, z, lane);

@@ -211,10 +211,10 @@ __global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const floa
   const bool chain = tid < 256;
   const int lt = tid & 255, k = lt >> 2, q = lt & 3;
   const int R = d.R, A = d.A, T = d.T;
-  __shared__ float dgh_s[2][RW][G3];
-  __shared__ float dgi_s[2][RW][G3];
-  __shared__ float hp_s[2][RW][H];
-  __shared__ float x1_s[2][RW][H];
+  // Per row and step: gh_s = [dgh (3H) | h_{t-1} (H)], gi_s = [dgi (3H) | x1 (H)]; one 4H record each, so the
+  // lane-split RW == 1 path writes component q of both with one unconditional LDS store per lane.
+  __shared__ float gh_s[2][RW][4 * H];
+  __shared__ float gi_s[2][RW][4 * H];
   __shared__ float dch_s[2][RW];   // per row: dLoss/dchosen (0 at t = T) and its action, for the fc2 grads
   __shared__ int act_s[2][RW];
   extern __shared__ float dyn[];   // W2 [A][H] | dW2 partial [A][H] | db2 [A]
@@ -241,15 +241,28 @@ __global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const floa
   const int64_t* arow[RL];   // &actions[ep(b)][0][agent], stride n per step
 #pragma unroll
   for (int ii = 0; ii < RL; ++ii) {
-    const int i = 4 * ii + q, r = r0 + i;
-    rv[ii] = i < RW && r < R;
+    const int i = RW == 1 ? 0 : 4 * ii + q, r = r0 + i;   // RW == 1: all four lanes of a quad share the row
+    rv[ii] = (RW == 1 || i < RW) && r < R;
     rr[ii] = min(r, R - 1);
     const int b = (int)fdiv((uint32_t)rr[ii], d.dN), ag = rr[ii] - b * d.n;
     arow[ii] = rp.actions + rp.ep(b) * d.t_stride * d.n + ag;
   }
   auto load = [&](int t, BwdIn (&s)[RL]) {
-    const int tc = max(t, 0);
+    const int tc = (VAR & 4) ? d.Tp - 1 : max(t, 0);   // VAR bit 4 (microbenchmark): cache-resident inputs
     const int td = min(tc, T - 1);
+    if constexpr (RW == 1) {
+      // lane-split: lane q loads gate component q and one of (h_{t-1}, x1, dch, action) — two loads per lane, no
+      // branches (divergent loads would blur the vmcnt bookkeeping the prefetch relies on). The action is read as
+      // the low word of the int64 (little-endian, 0 <= a < A).
+      const int64_t tr = (int64_t)tc * R + rr[0];
+      const float* src = q == 0   ? w.Hs + (tc > 0 ? tr - R : tr) * H + k
+                         : q == 1 ? w.X1 + tr * H + k
+                         : q == 2 ? w.dch + (int64_t)td * R + rr[0]
+                                  : (const float*)(arow[0] + (int64_t)tc * d.n);
+      s[0].gr = w.Gates[tr * (4 * H) + q * H + k];
+      s[0].hp = *src;
+      return;
+    }
 #pragma unroll
     for (int ii = 0; ii < RL; ++ii) {
       const int64_t tr = (int64_t)tc * R + rr[ii];
@@ -263,13 +276,39 @@ __global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const floa
   };
 
   float carry[RL];
-  float dbi0 = 0, dbi1 = 0, dbi2 = 0, dbh2 = 0;
+  float dbi0 = 0, dbi1 = 0, dbi2 = 0, dbh2 = 0;   // RW == 1: dbi0 / dbh2 hold this lane's component q of b_ih / b_hh
 #pragma unroll
   for (int ii = 0; ii < RL; ++ii) carry[ii] = 0.0f;
 
   auto chain_pre = [&](int t, const BwdIn (&cur)[RL], BwdIn (&nxt)[RL], float (&cz)[RL]) {
     load(t - 1, nxt);   // previous (earlier) step's inputs, in flight under this step
     const int pb = t & 1;
+    if constexpr (RW == 1) {
+      // lane-split: every lane of the quad gets the unit's inputs by DPP broadcast and computes the (cheap) gate
+      // derivatives redundantly; lane q then owns component q of every store.
+      const bool live = rv[0];
+      const float g = cur[0].gr, aux = cur[0].hp;
+      const float gr = quad_bcast<0>(g), gz = quad_bcast<1>(g), gn = quad_bcast<2>(g), ghn = quad_bcast<3>(g);
+      const float hp = t > 0 ? quad_bcast<0>(aux) : 0.0f, x1 = quad_bcast<1>(aux);
+      const float dchv = (live && t < T) ? quad_bcast<2>(aux) : 0.0f;
+      const int a = __builtin_bit_cast(int, quad_bcast<3>(aux));
+      const float dh = carry[0] + dchv * w2_s[a * H + k];
+      if (k == 0 && q == 0) { dch_s[pb][0] = dchv; act_s[pb][0] = a; }
+      const float dn = dh * (1.0f - gz);
+      const float dz = dh * (hp - gn);
+      const float dan = dn * (1.0f - gn * gn);
+      const float dar = (dan * ghn) * (gr * (1.0f - gr));
+      const float daz = dz * (gz * (1.0f - gz));
+      const float mine_i = q == 0 ? dar : (q == 1 ? daz : dan);   // dgi component q
+      const float mine_h = q == 2 ? dan * gr : mine_i;             // dgh component q
+      gi_s[pb][0][q * H + k] = q < 3 ? mine_i : x1;
+      gh_s[pb][0][q * H + k] = q < 3 ? mine_h : hp;
+      if (live && q < 3) w.dGI[((int64_t)t * R + rr[0]) * G3 + q * H + k] = mine_i;
+      dbi0 += q < 3 ? mine_i : 0.0f;
+      dbh2 += q < 3 ? mine_h : 0.0f;
+      cz[0] = dh * gz;
+      return;
+    }
 #pragma unroll
     for (int ii = 0; ii < RL; ++ii) {
       const int i = 4 * ii + q;
@@ -293,10 +332,10 @@ __global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const floa
         float* o = w.dGI + ((int64_t)t * R + rr[ii]) * G3;
         o[k] = dar; o[H + k] = daz; o[2 * H + k] = dan;
       }
-      dgi_s[pb][i][k] = dar; dgi_s[pb][i][H + k] = daz; dgi_s[pb][i][2 * H + k] = dan;
-      dgh_s[pb][i][k] = dar; dgh_s[pb][i][H + k] = daz; dgh_s[pb][i][2 * H + k] = dan * gr;
-      hp_s[pb][i][k] = hp;
-      x1_s[pb][i][k] = x1;
+      gi_s[pb][i][k] = dar; gi_s[pb][i][H + k] = daz; gi_s[pb][i][2 * H + k] = dan;
+      gh_s[pb][i][k] = dar; gh_s[pb][i][H + k] = daz; gh_s[pb][i][2 * H + k] = dan * gr;
+      gh_s[pb][i][G3 + k] = hp;
+      gi_s[pb][i][G3 + k] = x1;
       dbi0 += dar; dbi1 += daz; dbi2 += dan; dbh2 += dan * gr;
       cz[ii] = dh * gz;
     }
@@ -306,7 +345,7 @@ __global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const floa
     float s[RW];
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
-      const f32x4* dg4 = (const f32x4*)(&dgh_s[pb][i][48 * q]);
+      const f32x4* dg4 = (const f32x4*)(&gh_s[pb][i][48 * q]);
       float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
 #pragma unroll
       for (int c4 = 0; c4 < 12; ++c4) {
@@ -317,29 +356,37 @@ __global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const floa
       }
       s[i] = quad_sum((a0 + a1) + (a2 + a3));
     }
+    if constexpr (RW == 1) {
+      carry[0] = cz[0] + s[0];   // every lane of the quad keeps the unit's carry
+    } else {
 #pragma unroll
-    for (int ii = 0; ii < RL; ++ii) carry[ii] = cz[ii] + pick_row<RW>(s, ii, q);
+      for (int ii = 0; ii < RL; ++ii) carry[ii] = cz[ii] + pick_row<RW>(s, ii, q);
+    }
   };
+  float h_next[RW];   // accumulator waves: h_t[k] of each row, read at step t+1
+#pragma unroll
+  for (int i = 0; i < RW; ++i) h_next[i] = 0.0f;
   auto accumulate = [&](int t) {
     const int pb = t & 1;
     // fc2 grads: dW2[a][k] += dchosen * h_t[k]; (a, k) is owned by lane (k, q = a % 4), so no two lanes ever
-    // update the same word. h_t is the hp_s of step t+1 (still intact: that buffer is rewritten at step t-1).
+    // update the same word. h_t was the h_{t-1} record of step t+1, kept in a register since accumulate(t+1).
     if (t < T) {
 #pragma unroll
       for (int i = 0; i < RW; ++i) {
         const int a = act_s[pb][i];
         if ((a & 3) == q) {
           const float dchv = dch_s[pb][i];
-          dw2_s[a * H + k] += dchv * hp_s[pb ^ 1][i][k];
+          dw2_s[a * H + k] += dchv * h_next[i];
           if (k == 0) db2_s[a] += dchv;
         }
       }
     }
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
-      const f32x4* dg4 = (const f32x4*)(&dgh_s[pb][i][48 * q]);
-      const f32x4* di4 = (const f32x4*)(&dgi_s[pb][i][48 * q]);
-      const float hpk = hp_s[pb][i][k], x1k = x1_s[pb][i][k];
+      const f32x4* dg4 = (const f32x4*)(&gh_s[pb][i][48 * q]);
+      const f32x4* di4 = (const f32x4*)(&gi_s[pb][i][48 * q]);
+      const float hpk = gh_s[pb][i][G3 + k], x1k = gi_s[pb][i][G3 + k];
+      h_next[i] = hpk;
 #pragma unroll
       for (int c4 = 0; c4 < 12; ++c4) {
         const f32x4 dg = dg4[c4], di = di4[c4];
@@ -351,26 +398,49 @@ __global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const floa
       }
     }
   };
-  auto step = [&](int t, const BwdIn (&cur)[RL], BwdIn (&nxt)[RL]) {
-    float cz[RL];
-    if (chain) chain_pre(t, cur, nxt, cz);
+  // The two roles run separate loops that meet at one barrier per step: chain_pre(t) writes record buffer t & 1,
+  // the barrier publishes it, then chain_post(t) and accumulate(t) both read it while chain_pre(t-1) fills the
+  // other buffer (rewritten only after the next barrier, which accumulate(t) reaches first).
+  uint64_t cyc_pre = 0, cyc_bar = 0, cyc_post = 0;   // VAR bit 2 (microbenchmark): chain section cycle stamps
+  if (chain) {
+    __builtin_amdgcn_s_setprio(2);
+    BwdIn sa[RL], sb[RL];
+    load(d.Tp - 1, sa);
+    drain_vmem();
     lds_barrier();
-    if (chain) chain_post(t, cz);
-    else accumulate(t);
-  };
-
-  if (chain) __builtin_amdgcn_s_setprio(2);
-  BwdIn sa[RL], sb[RL];
-  if (chain) load(d.Tp - 1, sa);
-  drain_vmem();
-  lds_barrier();
-  int t = d.Tp - 1;
-  for (; t - 1 >= 0; t -= 2) {
-    step(t, sa, sb);
-    step(t - 1, sb, sa);
+    auto step = [&](int t, const BwdIn (&cur)[RL], BwdIn (&nxt)[RL]) {
+      float cz[RL];
+      uint64_t c0 = 0, c1 = 0, c2 = 0;
+      if (VAR & 2) c0 = __builtin_amdgcn_s_memtime();
+      chain_pre(t, cur, nxt, cz);
+      if (VAR & 2) c1 = __builtin_amdgcn_s_memtime();
+      lds_barrier();
+      if (VAR & 2) c2 = __builtin_amdgcn_s_memtime();
+      chain_post(t, cz);
+      if (VAR & 2) {
+        __builtin_amdgcn_s_waitcnt(0);   // keep the mat-vec inside the stamp
+        const uint64_t c3 = __builtin_amdgcn_s_memtime();
+        cyc_pre += c1 - c0; cyc_bar += c2 - c1; cyc_post += c3 - c2;
+      }
+    };
+    int t = d.Tp - 1;
+    for (; t - 1 >= 0; t -= 2) {
+      step(t, sa, sb);
+      step(t - 1, sb, sa);
+    }
+    if (t >= 0) step(t, sa, sb);
+    __builtin_amdgcn_s_setprio(0);
+  } else {
+    lds_barrier();
+    for (int t = d.Tp - 1; t >= 0; --t) {
+      lds_barrier();
+      if (!(VAR & 8)) accumulate(t);   // VAR bit 8 (microbenchmark): chain alone
+    }
   }
-  if (t >= 0) step(t, sa, sb);
-  __builtin_amdgcn_s_setprio(0);
+  if ((VAR & 2) && tid == 0) {
+    uint64_t* st = (uint64_t*)w.slab_mix + 4 * blockIdx.x;
+    st[0] = cyc_pre; st[1] = cyc_bar; st[2] = cyc_post; st[3] = (uint64_t)__builtin_bit_cast(uint32_t, carry[0]);
+  }
 
   // per-workgroup partial slab
   float* slab = w.slab_rnn + (int64_t)blockIdx.x * slab_len;
@@ -384,10 +454,14 @@ __global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const floa
       slab[o_hh + (48 * q + c) * H + k] = accH[c];
     }
   } else {
-    dbi0 = quad_sum(dbi0); dbi1 = quad_sum(dbi1); dbi2 = quad_sum(dbi2); dbh2 = quad_sum(dbh2);
-    if (q == 0) {
-      slab[o_bi + k] = dbi0; slab[o_bi + H + k] = dbi1; slab[o_bi + 2 * H + k] = dbi2;
-      slab[o_bh + k] = dbi0; slab[o_bh + H + k] = dbi1; slab[o_bh + 2 * H + k] = dbh2;
+    if constexpr (RW == 1) {
+      if (q < 3) { slab[o_bi + q * H + k] = dbi0; slab[o_bh + q * H + k] = dbh2; }
+    } else {
+      dbi0 = quad_sum(dbi0); dbi1 = quad_sum(dbi1); dbi2 = quad_sum(dbi2); dbh2 = quad_sum(dbh2);
+      if (q == 0) {
+        slab[o_bi + k] = dbi0; slab[o_bi + H + k] = dbi1; slab[o_bi + 2 * H + k] = dbi2;
+        slab[o_bh + k] = dbi0; slab[o_bh + H + k] = dbi1; slab[o_bh + 2 * H + k] = dbh2;
+      }
     }
   }
   lds_barrier();

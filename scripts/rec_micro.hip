@@ -81,6 +81,18 @@ int main(int argc, char** argv) {
     return time_it([&] { hipLaunchKernelGGL(kern, dim3((d.R + rw - 1) / rw), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn); });
   };
   printf("bwd RW1 %.1f us\n", runb(gru_bwd_kernel<1, 0>, 1));
+  printf("bwd RW1 V4(cached inputs) %.1f us\n", runb(gru_bwd_kernel<1, 4>, 1));
+  printf("bwd RW1 V8(no accumulate) %.1f us\n", runb(gru_bwd_kernel<1, 8>, 1));
+  printf("bwd RW1 V12 %.1f us\n", runb(gru_bwd_kernel<1, 12>, 1));
+  for (int var : {2, 14}) {
+    if (var == 2) runb(gru_bwd_kernel<1, 2>, 1); else runb(gru_bwd_kernel<1, 14>, 1);
+    std::vector<uint64_t> st(4 * d.R);
+    CK(hipMemcpy(st.data(), w.slab_mix, st.size() * 8, hipMemcpyDeviceToHost));
+    double c[3] = {0, 0, 0};
+    for (int i = 0; i < d.R; ++i) for (int j = 0; j < 3; ++j) c[j] += st[4 * i + j];
+    printf("bwd RW1 V%d stamped cycles/step: pre %.0f barrier %.0f post %.0f\n", var, c[0] / d.R / d.Tp,
+           c[1] / d.R / d.Tp, c[2] / d.R / d.Tp);
+  }
   printf("bwd RW2 %.1f us\n", runb(gru_bwd_kernel<2, 0>, 2));
 
   return 0;
