@@ -93,7 +93,8 @@ int mq_set_data_parallel(mq_handle* h, int32_t on);
 int mq_update_targets(mq_handle* h, void* stream);
 
 /* Copy an intermediate of the last mq_forward_backward into dst (device): 0 = online mac_out [t][b*n+a][A],
- * 1 = target mac_out (same layout), 2 = dQ/dchosen [t][b*n+a] (unnormalised). Returns element count in *count. */
+ * 1 = target mac_out (same layout), 2 = dQ/dchosen [t][b*n+a] (unnormalised), 3 = online relu(fc1) activations
+ * [t][b*n+a][64]. Returns element count in *count. */
 int mq_copy_intermediate(mq_handle* h, int which, float* dst, int64_t* count, void* stream);
 
 /* BasicMAC.forward(ep_batch, t) for every episode of `batch`: h_in/h_out [batch*n][64] (h_in may equal

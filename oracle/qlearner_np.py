@@ -59,10 +59,13 @@ def build_inputs(obs_t, onehot_prev, n_agents):
     return np.concatenate([obs_t, onehot_prev, eye], -1).reshape(B * n_agents, -1).astype(F32)
 
 
-def agent_unroll(p, obs, actions_onehot, keep_cache=False):
+def agent_unroll(p, obs, actions_onehot, keep_cache=False, relu_mask=None, pre_out=None):
     """BasicMAC.forward over t = 0..T (q_learner.py:47-52 / 58-62) with RNNAgent (rnn_agent.py:27-36).
 
     obs (B,Tp,n,O), actions_onehot (B,Tp,n,A) -> mac_out (B,Tp,n,A) [+ cache for the backward pass].
+    relu_mask (B,Tp,n,H) bool: take the fc1 relu's on/off decisions from another implementation (a parity test
+    following it through fc1 pre-activations that round to the other side of 0). pre_out: list receiving the
+    fc1 pre-activations per step.
     """
     B, Tp, n, _ = obs.shape
     A = actions_onehot.shape[-1]
@@ -72,7 +75,11 @@ def agent_unroll(p, obs, actions_onehot, keep_cache=False):
     for t in range(Tp):
         prev = np.zeros((B, n, A), F32) if t == 0 else actions_onehot[:, t - 1]
         x = build_inputs(obs[:, t], prev, n)
-        x1 = _relu(x @ p["fc1.weight"].T + p["fc1.bias"])
+        pre = x @ p["fc1.weight"].T + p["fc1.bias"]
+        if pre_out is not None:
+            pre_out.append(pre.reshape(B, n, -1))
+        on = pre > 0 if relu_mask is None else relu_mask[:, t].reshape(B * n, -1)
+        x1 = np.where(on, pre, F32(0.0)).astype(F32)
         gi = x1 @ p["rnn.weight_ih"].T + p["rnn.bias_ih"]
         gh = h @ p["rnn.weight_hh"].T + p["rnn.bias_hh"]
         r = _sigmoid(gh[:, :H] + gi[:, :H])
@@ -81,10 +88,22 @@ def agent_unroll(p, obs, actions_onehot, keep_cache=False):
         h_new = ((h - nn_) * z + nn_).astype(F32)
         q = h_new @ p["fc2.weight"].T + p["fc2.bias"]
         if keep_cache:
-            cache.append((x, x1, h, r, z, nn_, gh[:, 2 * H:].copy(), h_new))
+            cache.append((x, x1, on, h, r, z, nn_, gh[:, 2 * H:].copy(), h_new))
         h = h_new
         outs.append(q.reshape(B, n, A))
     return np.stack(outs, 1).astype(F32), cache
+
+
+def fc1_preacts(p, obs, actions_onehot):
+    """fc1 pre-activations of every (b, t, agent) (rnn_agent.py:28 before the relu): (B,Tp,n,H)."""
+    B, Tp, n, _ = obs.shape
+    A = actions_onehot.shape[-1]
+    out = []
+    for t in range(Tp):
+        prev = np.zeros((B, n, A), F32) if t == 0 else actions_onehot[:, t - 1]
+        x = build_inputs(obs[:, t], prev, n)
+        out.append((x @ p["fc1.weight"].T + p["fc1.bias"]).reshape(B, n, -1))
+    return np.stack(out, 1).astype(F32)
 
 
 def qmix_forward(mp, agent_qs, states, n_agents, keep_cache=False):
@@ -141,7 +160,7 @@ def agent_backward(p, cache, dmac_out):
     g = OrderedDict((k, np.zeros_like(v)) for k, v in p.items())
     dh = np.zeros((B * n, H), F32)
     for t in range(Tp - 1, -1, -1):
-        x, x1, h_prev, r, z, nn_, ghn, h_new = cache[t]
+        x, x1, on, h_prev, r, z, nn_, ghn, h_new = cache[t]
         dq = dmac_out[:, t].reshape(B * n, A)
         g["fc2.weight"] += dq.T @ h_new
         g["fc2.bias"] += dq.sum(0)
@@ -157,7 +176,7 @@ def agent_backward(p, cache, dmac_out):
         g["rnn.bias_ih"] += dgi.sum(0)
         g["rnn.weight_hh"] += dgh.T @ h_prev
         g["rnn.bias_hh"] += dgh.sum(0)
-        dx1 = (dgi @ p["rnn.weight_ih"]) * (x1 > 0)
+        dx1 = (dgi @ p["rnn.weight_ih"]) * on
         g["fc1.weight"] += dx1.T @ x
         g["fc1.bias"] += dx1.sum(0)
         dh = (dh * z + dgh @ p["rnn.weight_hh"]).astype(F32)
@@ -196,11 +215,12 @@ class OracleQLearner:
         self.log_stats_t = -self.cfg.get("learner_log_interval", 0) - 1
         self.last = {}
 
-    def forward(self, batch, keep_cache=False, cur_max_override=None):
+    def forward(self, batch, keep_cache=False, cur_max_override=None, relu_override=None):
         """q_learner.py:39-97: returns dict of intermediates (+ caches).
 
         cur_max_override (B, T, n): use these double-Q argmax actions instead of recomputing them — lets a parity
         test follow the other implementation through near-tie argmax flips (both choices are correct fp32 ties).
+        relu_override (B, T+1, n, H) bool: the online agent's fc1 relu decisions, likewise (see agent_unroll).
         """
         c = self.cfg
         n = c["n_agents"]
@@ -210,7 +230,7 @@ class OracleQLearner:
         mask = batch["filled"][:, :-1].astype(F32).copy()
         mask[:, 1:] = mask[:, 1:] * (F32(1.0) - terminated[:, :-1])
         avail = batch["avail_actions"]
-        mac_out, acache = agent_unroll(self.p, batch["obs"], batch["actions_onehot"], keep_cache)
+        mac_out, acache = agent_unroll(self.p, batch["obs"], batch["actions_onehot"], keep_cache, relu_override)
         chosen = np.take_along_axis(mac_out[:, :-1], actions, axis=3)[..., 0]
         tmo_full, _ = agent_unroll(self.tp, batch["obs"], batch["actions_onehot"])
         tmo = tmo_full[:, 1:].copy()
@@ -244,10 +264,11 @@ class OracleQLearner:
                     target_max=target_max, q_tot=q_tot, target_q_tot=tq_tot, targets=targets, td=td, mask=m,
                     mask_sum=msum, loss=float(loss), acache=acache, mcache=mcache, actions=actions)
 
-    def gradients(self, batch, fw=None, cur_max_override=None):
+    def gradients(self, batch, fw=None, cur_max_override=None, relu_override=None):
         """Unclipped gradients of the loss (agent params then mixer params, reference order)."""
         c = self.cfg
-        fw = fw or self.forward(batch, keep_cache=True, cur_max_override=cur_max_override)
+        fw = fw or self.forward(batch, keep_cache=True, cur_max_override=cur_max_override,
+                                relu_override=relu_override)
         td, m, msum = fw["td"], fw["mask"], fw["mask_sum"]
         dq_tot = ((F32(2.0) * (td * m)) * (F32(1.0) / msum)) * m            # d/dQ_tot of sum((td*m)^2)/sum(m)
         B, T = td.shape[:2]
@@ -268,10 +289,10 @@ class OracleQLearner:
         ag = agent_backward(self.p, fw["acache"], dmac)
         return ag, mg, fw
 
-    def train(self, batch, t_env, episode_num, cur_max_override=None):
+    def train(self, batch, t_env, episode_num, cur_max_override=None, relu_override=None):
         """q_learner.py:37-116; returns the stats dict it would log."""
         c = self.cfg
-        ag, mg, fw = self.gradients(batch, cur_max_override=cur_max_override)
+        ag, mg, fw = self.gradients(batch, cur_max_override=cur_max_override, relu_override=relu_override)
         grads = OrderedDict(list(ag.items()) + list(mg.items()))
         grad_norm = clip_grad_norm(grads, c["grad_norm_clip"])
         params = OrderedDict(list(self.p.items()) + list(self.mp.items()))

@@ -1,0 +1,387 @@
+// Fused agent forward for one-row workgroups: fc1 -> relu -> W_ih (MFMA) feeding the GRU recurrence (VALU), with
+// fc2 (MFMA) behind it — rnn_agent.py:24-28 for every (t, row) of QLearner.train's unroll (q_learner.py:49-52,
+// 60-62), online and target net in one grid (blockIdx.y).
+//
+// The recurrence is VALU-issue bound (W_hh in VGPRs, DPP quad reductions, one LDS barrier per step) and leaves the
+// matrix cores idle, so the row-parallel contractions around it run on MFMA in the same workgroup, 16 steps at a
+// time (the MFMA M dimension is time). 512 threads, two wave roles meeting at the one barrier per step:
+//  * recurrence waves (0-3, s_setprio 2): the h chain exactly as gru_fwd_body<1>, but with the step's input gates
+//    read from LDS (no global loads at all: nothing for vmcnt to serialise on);
+//  * producer waves (4-7): per chunk c of the T loop (p = t & 15), for chunk c+1 and c-1
+//      p = 0        fc2 of chunk c-1: Q[16][A] = H[16][64] W2^T + b2   (hidden-state history in LDS)
+//      p = 1        issue chunk c+1's obs gather (registers; consumed 4 steps later)
+//      p = 5, 6     stage chunk c+1's agent inputs in LDS: obs rows, last-action / agent-id one-hots
+//      p = 7 .. 10  fc1 of chunk c+1: X1[16][64] = relu(XIN[16][I] W1^T + b1)
+//      p = 11 .. 15 W_ih of chunk c+1: GI[16][192] = X1 W_ih^T + b_ih  -> LDS, read by chunk c+1's steps
+//    unrolled over p so each phase is straight-line code (the gather's vmcnt wait is exact). At most 12
+//    v_mfma_f32_16x16x4_f32 per producer wave and step: well inside one recurrence step.
+// X1 / XIN (online net, for the backward pass) and Q leave as 16-row tiles; of the target net only Q is written.
+//
+// MFMA operand maps (v_mfma_f32_16x16x4_f32, lane l, g = l >> 4, c = l & 15): A[i = c][kk = g],
+// B[kk = g][j = c], D[i = 4g + reg][j = c]. Lane group g owns a contiguous quarter of K (k = g * Kq + kb), so
+// A and B fragments are row-contiguous LDS reads (W_ih's fragments stay in VGPRs).
+#pragma once
+#include "gru_kernels.hpp"
+
+namespace mq {
+
+constexpr int FCH = 16;            // steps per chunk
+constexpr int FKQ = 28;            // fc1 k-blocks per lane group: I <= 112
+constexpr int FXP = 4 * FKQ + 4;   // xin / w1 pitch
+constexpr int FGATHER = 8;         // obs gather slots per producer thread: 16 * O <= 2048
+
+MQ_DEV f32x4 mfma16x4(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+// Hide a value's provenance from the optimiser so address math derived from it is recomputed where it is used
+// instead of being hoisted out of the chunk loop (and spilled: the producer waves run at 128 VGPRs).
+MQ_DEV int opaque(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// Host-side eligibility of the fused path.
+inline bool fused_fwd_ok(int I, int O, int A, int n, int64_t RT) {
+  return I <= 4 * FKQ && O <= 128 && A <= 16 && n * O < (1 << 16) && RT * I < (int64_t(1) << 31);
+}
+
+struct FusedLds {
+  float hbuf[2][H];
+  float hs[2][FCH][H + 4];   // h history of the last two chunks (fc2 operand)
+  float gi[2][FCH][G3];      // input gates of the current / next chunk
+  float xin[FCH][FXP];       // agent inputs of the next chunk, zero-padded to 4 * Kq
+  float x1[FCH][H + 4];
+  float w1[H][FXP];          // fc1 weight [64][I], zero-padded
+  float w2[16][H + 4];       // fc2 weight [A <= 16][64], zero-padded
+  int aprev[FCH];
+};
+
+// VAR: ablation bits for scripts/rec_micro.hip only (production = 0): 1 skip Hs/Gates stores, 2 stamp the T loop,
+// 4 producers idle (recurrence alone on stale gates), 8 per-phase cycle bins.
+template <int VAR = 0>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void gru_fwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P0,
+                                                               const float* __restrict__ P1, Lay L, Work w) {
+  __shared__ FusedLds S;
+  const int z = blockIdx.y;
+  const bool online = z == 0;
+  const float* __restrict__ P = z ? P1 : P0;
+  const int tid = threadIdx.x;
+  const bool rec = tid < 256;
+  const int R = d.R, Tp = d.Tp, I = d.I, O = d.O, A = d.A, n = d.n;
+  const int cl = (Tp - 1) / FCH;   // last chunk
+  const int r = blockIdx.x;
+
+  // ---- shared prologue: weights to LDS, zero padding, h0
+  for (int e = tid; e < H * FXP; e += 512) {
+    const int nn = e / FXP, k = e - nn * FXP;
+    S.w1[nn][k] = k < I ? P[L.o[MQ_P_FC1_W] + (int64_t)nn * I + k] : 0.0f;
+  }
+  for (int e = tid; e < 16 * (H + 4); e += 512) {
+    const int a = e / (H + 4), k = e - a * (H + 4);
+    S.w2[a][k] = (a < A && k < H) ? P[L.o[MQ_P_FC2_W] + (int64_t)a * H + k] : 0.0f;
+  }
+  for (int e = tid; e < FCH * FXP; e += 512) (&S.xin[0][0])[e] = 0.0f;
+  if (tid < H) S.hbuf[0][tid] = 0.0f;   // init_hidden: h0 = 0
+
+  if (rec) {
+    // ================================================================ recurrence waves
+    const int j = tid >> 2, q = tid & 3;
+    float wr[16], wz[16], wn[16];
+    {
+      const float* Whh = P + L.o[MQ_P_RNN_W_HH];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        wr[k] = Whh[(0 * H + j) * H + 16 * q + k];
+        wz[k] = Whh[(1 * H + j) * H + 16 * q + k];
+        wn[k] = Whh[(2 * H + j) * H + 16 * q + k];
+      }
+    }
+    const float bhr = P[L.o[MQ_P_RNN_B_HH] + j], bhz = P[L.o[MQ_P_RNN_B_HH] + H + j],
+                bhn = P[L.o[MQ_P_RNN_B_HH] + 2 * H + j];
+    drain_vmem();
+    for (int i = 0; i < 5; ++i) lds_barrier();   // the producers' chunk-0 prologue (5 barriers)
+    __builtin_amdgcn_s_setprio(2);
+    float* Hz = w.Hs;   // online only: the backward pass reads h_{t-1}
+    const int gcol = min(q, 2) * H + j;
+    float own = S.gi[0][0][gcol];   // this step's input gate, read right after the previous step's barrier
+    auto step = [&](int t) {
+      const int p = t & (FCH - 1), c = t / FCH;
+      const float* hb = S.hbuf[t & 1];
+      float sr, sz, sn;
+      {
+        const f32x4* hv4 = (const f32x4*)(&hb[16 * q]);
+        float ar = 0.0f, az = 0.0f, an = 0.0f, ar2 = 0.0f, az2 = 0.0f, an2 = 0.0f;
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+          const f32x4 hv = hv4[k4];
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            const int k = 4 * k4 + e;
+            ar = fmaf(wr[k], hv[e], ar); ar2 = fmaf(wr[k + 1], hv[e + 1], ar2);
+            az = fmaf(wz[k], hv[e], az); az2 = fmaf(wz[k + 1], hv[e + 1], az2);
+            an = fmaf(wn[k], hv[e], an); an2 = fmaf(wn[k + 1], hv[e + 1], an2);
+          }
+        }
+        sr = quad_sum(ar + ar2);
+        sz = quad_sum(az + az2);
+        sn = quad_sum(an + an2);
+      }
+      // lane-split gate math (as gru_fwd_body<1>): lane 0 r, lane 1 z, lane 2 n; lane q stores component q
+      const float gh = q == 0 ? sr + bhr : (q == 1 ? sz + bhz : 0.0f);
+      const float sg = sigm_fast(gh + own);
+      const float rg = quad_bcast<0>(sg), zg = quad_bcast<1>(sg);
+      const float ghn = sn + bhn;
+      const float ng = quad_bcast<2>(tanh_fast(own + ghn * rg));
+      const float hp = hb[j];
+      const float h1 = (hp - ng) * zg + ng;   // ATen gru_cell: (hx - n) * z + n
+      if (q == 0) S.hbuf[(t + 1) & 1][j] = h1;
+      if (q == 1) S.hs[c & 1][p][j] = h1;
+      if (online && !(VAR & 1)) {
+        const int64_t tr = (int64_t)t * R + r;
+        if (q == 0) Hz[tr * H + j] = h1;
+        w.Gates[tr * (4 * H) + q * H + j] = q == 0 ? rg : (q == 1 ? zg : (q == 2 ? ng : ghn));
+      }
+      lds_barrier();
+      const int t1 = t + 1;
+      own = S.gi[(t1 / FCH) & 1][t1 & (FCH - 1)][gcol];
+    };
+    uint64_t c0 = 0, r0t = 0;
+    if (VAR & 2) { c0 = __builtin_amdgcn_s_memtime(); r0t = __builtin_amdgcn_s_memrealtime(); }
+    if (VAR & 8) {   // diagnostic only: shader cycles per step phase p, summed over the chunks
+      uint64_t bins[FCH];
+#pragma unroll
+      for (int i = 0; i < FCH; ++i) bins[i] = 0;
+      for (int t = 0; t < Tp; ++t) {
+        const uint64_t a = __builtin_amdgcn_s_memtime();
+        step(t);
+        const uint64_t e = __builtin_amdgcn_s_memtime();
+#pragma unroll
+        for (int i = 0; i < FCH; ++i)
+          if (i == (t & (FCH - 1))) bins[i] += e - a;
+      }
+      if (tid == 0) {
+#pragma unroll
+        for (int i = 0; i < FCH; ++i)
+          ((uint64_t*)w.slab_mix)[FCH * (blockIdx.y * gridDim.x + blockIdx.x) + i] = bins[i];
+      }
+    } else {
+      for (int t = 0; t < Tp; ++t) step(t);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if ((VAR & 2) && tid == 0) {   // diagnostic only: shader cycles and 100 MHz ticks of the whole T loop
+      const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+      ((uint64_t*)w.slab_mix)[2 * (blockIdx.y * gridDim.x + blockIdx.x)] = c1 - c0;
+      ((uint64_t*)w.slab_mix)[2 * (blockIdx.y * gridDim.x + blockIdx.x) + 1] = r1 - r0t;
+    }
+    return;
+  }
+
+  // ================================================================== producer waves
+  const int ptid = tid - 256, wv = ptid >> 6, lane = ptid & 63, g = lane >> 4, c16 = lane & 15;
+  const int Kq = (I + 15) / 16 * 4;   // k-blocks per lane group (multiple of 4: b128 operand reads)
+  float wih[3][16], bih[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int nn = 16 * (3 * wv + s) + c16;
+    const float* Wi = P + L.o[MQ_P_RNN_W_IH] + (int64_t)nn * H + 16 * g;
+#pragma unroll
+    for (int kb = 0; kb < 16; ++kb) wih[s][kb] = Wi[kb];
+    bih[s] = P[L.o[MQ_P_RNN_B_IH] + nn];
+  }
+  const float b1 = P[L.o[MQ_P_FC1_B] + 16 * wv + c16];
+  const float b2 = c16 < A ? P[L.o[MQ_P_FC2_B] + c16] : 0.0f;
+
+  // replay addressing of this row (r = b * n + agent)
+  const int b = (int)fdiv((uint32_t)r, d.dN), ag = r - b * n;
+  const int64_t slot0 = rp.ep(b) * d.t_stride;
+  const float* obs_row = rp.obs + (slot0 * n + ag) * (int64_t)O;   // + t * n * O
+  float* X1o = w.X1;     // online X1 [RT][H]
+  float* XINo = w.XIN;   // online XIN [RT][I]
+  float* Qz = w.Q + (int64_t)z * d.RT() * A;
+
+  // gather slot s: element e = ptid + 256 s of the chunk's [16][O] obs block -> (row i, column), packed once as
+  // (i << 16) | (i * n * O + column) (the element's offset from the chunk's first obs row); -1 past the block
+  int gsl[FGATHER];
+#pragma unroll
+  for (int s = 0; s < FGATHER; ++s) {
+    const int e = ptid + 256 * s, i = e / O;
+    gsl[s] = e < FCH * O ? (i << 16) | (i * n * O + e - i * O) : -1;
+  }
+  const int nO = n * O;
+  float xr[FGATHER];
+  int f_ld = 0, a_ld = -1;   // low words of filled[t-1] / actions[t-1] (int64, little-endian, small values)
+  auto issue_gather = [&](int cc) {
+    const int t0 = FCH * cc;
+    // unconditional loads from clamped addresses (no exec-masked branches); out-of-range slots are zeroed when
+    // stored (store_gather)
+    const float* base = obs_row + (int64_t)t0 * nO;
+    const int lim = (Tp - 1 - t0) * nO + O - 1;   // last valid element offset of this chunk
+#pragma unroll
+    for (int s = 0; s < FGATHER; ++s) xr[s] = base[min(opaque(gsl[s]) & 0xFFFF, lim)];
+    {
+      const int t = min(max(t0 + (ptid & (FCH - 1)), 1), Tp - 1) - 1;
+      f_ld = *(const int*)(rp.filled + slot0 + t);
+      a_ld = *(const int*)(rp.actions + (slot0 + t) * n + ag);
+    }
+  };
+  auto store_gather = [&](int cc) {
+    const int t0 = FCH * cc;
+    float* xg = XINo + ((int64_t)t0 * R + r) * I;
+#pragma unroll
+    for (int s = 0; s < FGATHER; ++s) {
+      const int gs = opaque(gsl[s]);
+      if (gs < 0) continue;
+      const int i = gs >> 16, col = (gs & 0xFFFF) - i * nO;
+      const bool ok = t0 + i < Tp;
+      S.xin[i][col] = ok ? xr[s] : 0.0f;
+      if (online && ok) xg[i * R * I + col] = xr[s];   // RT * I < 2^31 (host check)
+    }
+    // actions_onehot[t-1] is zero unless slot t-1 was filled (runner contract)
+    if (ptid < FCH) {
+      const int t = t0 + ptid;
+      S.aprev[ptid] = (d.last_action && t > 0 && t < Tp && f_ld) ? a_ld : -1;
+    }
+  };
+  auto onehots = [&](int cc) {
+    const int t0 = FCH * cc, wd = I - O, i = ptid >> 4, t = t0 + i;
+    for (int col = ptid & 15; col < wd; col += 16) {
+      float v;
+      if (d.last_action && col < A) v = col == S.aprev[i] ? 1.0f : 0.0f;
+      else v = (col - (d.last_action ? A : 0)) == ag ? 1.0f : 0.0f;
+      S.xin[i][O + col] = v;
+      if (online && t < Tp) XINo[((int64_t)t * R + r) * I + O + col] = v;
+    }
+  };
+  f32x4 acc1 = {0, 0, 0, 0}, acc1b = {0, 0, 0, 0}, accg[3] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+  auto fc1_part = [&](int m0, int m1) {   // b128 groups [m0, m1) of this lane group's Kq k-blocks
+#pragma unroll
+    for (int m = m0; m < m1; ++m) {
+      if (4 * m >= Kq) break;
+      const f32x4 av = *(const f32x4*)&S.xin[c16][g * Kq + 4 * m];
+      const f32x4 bv = *(const f32x4*)&S.w1[16 * wv + c16][g * Kq + 4 * m];
+      acc1 = mfma16x4(av[0], bv[0], acc1);
+      acc1b = mfma16x4(av[1], bv[1], acc1b);
+      acc1 = mfma16x4(av[2], bv[2], acc1);
+      acc1b = mfma16x4(av[3], bv[3], acc1b);
+    }
+  };
+  auto fc1_epi = [&](int cc) {
+    const int t0 = FCH * cc;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = 4 * g + e, t = t0 + i;
+      const float x = fmaxf((acc1[e] + acc1b[e]) + b1, 0.0f);
+      S.x1[i][16 * wv + c16] = x;
+      if (online && t < Tp) X1o[((int64_t)t * R + r) * H + 16 * wv + c16] = x;
+    }
+    acc1 = f32x4{0, 0, 0, 0};
+    acc1b = f32x4{0, 0, 0, 0};
+  };
+  auto gi_part = [&](int k0, int k1) {    // k-blocks [k0, k1) of this lane group's 16
+#pragma unroll
+    for (int kb = k0; kb < k1; ++kb) {
+      const float av = S.x1[c16][16 * g + kb];
+#pragma unroll
+      for (int s = 0; s < 3; ++s) accg[s] = mfma16x4(av, wih[s][kb], accg[s]);
+    }
+  };
+  auto gi_epi = [&](int cc) {
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) S.gi[cc & 1][4 * g + e][16 * (3 * wv + s) + c16] = accg[s][e] + bih[s];
+      accg[s] = f32x4{0, 0, 0, 0};
+    }
+  };
+  // fc2 of a chunk in two steps: every producer wave multiplies its 16-wide K quarter (4 MFMAs) into a partial
+  // tile in LDS (aliasing x1, idle at p = 0, 1); wave 0 sums the four partials and stores Q.
+  float(*qpart)[FCH][16] = (float(*)[FCH][16])&S.x1[0][0];   // [4 waves][16 steps][16 actions]
+  auto fc2_partial = [&](int cc) {
+    f32x4 acc2 = {0, 0, 0, 0};
+    const f32x4 av = *(const f32x4*)&S.hs[cc & 1][c16][16 * wv + 4 * g];
+    const f32x4 bv = *(const f32x4*)&S.w2[c16][16 * wv + 4 * g];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc2 = mfma16x4(av[e], bv[e], acc2);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) qpart[wv][4 * g + e][c16] = acc2[e];
+  };
+  auto fc2_store = [&](int cc) {
+    if (wv != 0) return;
+    const int t0 = FCH * cc;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = 4 * g + e, t = t0 + i;
+      const float v = ((qpart[0][i][c16] + qpart[1][i][c16]) + (qpart[2][i][c16] + qpart[3][i][c16])) + b2;
+      if (t < Tp && c16 < A) Qz[((int64_t)t * R + r) * A + c16] = v;
+    }
+  };
+
+  // chunk 0 synchronously (5 barriers, matched by the recurrence waves)
+  issue_gather(0);
+  drain_vmem();
+  lds_barrier();   // 1: weights, padding staged
+  store_gather(0);
+  lds_barrier();   // 2
+  onehots(0);
+  lds_barrier();   // 3
+  fc1_part(0, FKQ / 4);
+  fc1_epi(0);
+  lds_barrier();   // 4
+  gi_part(0, 16);
+  gi_epi(0);
+  lds_barrier();   // 5
+
+  if (!(VAR & 4)) {
+    for (int c = 0; c <= cl; ++c) {
+      const int t0 = FCH * c;
+      const bool next = c + 1 <= cl;
+#pragma unroll
+      for (int p = 0; p < FCH; ++p) {
+        if (t0 + p >= Tp) continue;   // last chunk: no work past Tp (no work for chunk c+1 either)
+        if (p == 0) {
+          if (c >= 1) fc2_partial(c - 1);
+          if (next) issue_gather(c + 1);
+        }
+        if (p == 1 && c >= 1) fc2_store(c - 1);
+        if (next) {
+          if (p == 5) store_gather(c + 1);
+          if (p == 6) onehots(c + 1);
+          if (p == 7) fc1_part(0, 2);
+          if (p == 8) fc1_part(2, 4);
+          if (p == 9) fc1_part(4, 6);
+          if (p == 10) { fc1_part(6, 8); fc1_epi(c + 1); }
+          if (p == 11) gi_part(0, 4);
+          if (p == 12) gi_part(4, 7);
+          if (p == 13) gi_part(7, 10);
+          if (p == 14) gi_part(10, 13);
+          if (p == 15) { gi_part(13, 16); gi_epi(c + 1); }
+        }
+        lds_barrier();
+      }
+    }
+  } else {
+    for (int t = 0; t < Tp; ++t) lds_barrier();
+  }
+  // the last chunk (and the previous one's store when the last chunk is a single step) after the final barrier,
+  // in wave 0 alone
+  if (cl >= 1 && Tp - FCH * cl < 2) fc2_store(cl - 1);
+  if (wv == 0) {
+    f32x4 q0 = {0, 0, 0, 0}, q1 = {0, 0, 0, 0};
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const f32x4 av = *(const f32x4*)&S.hs[cl & 1][c16][16 * g + 4 * m];
+      const f32x4 bv = *(const f32x4*)&S.w2[c16][16 * g + 4 * m];
+      q0 = mfma16x4(av[0], bv[0], q0);
+      q1 = mfma16x4(av[1], bv[1], q1);
+      q0 = mfma16x4(av[2], bv[2], q0);
+      q1 = mfma16x4(av[3], bv[3], q1);
+    }
+    const int t0 = FCH * cl;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int t = t0 + 4 * g + e;
+      if (t < Tp && c16 < A) Qz[((int64_t)t * R + r) * A + c16] = (q0[e] + q1[e]) + b2;
+    }
+  }
+}
+
+}  // namespace mq

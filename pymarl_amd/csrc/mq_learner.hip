@@ -15,6 +15,7 @@
 //   --- (data-parallel all-reduce of the gradient buffer happens here, in the caller)
 //   apply    / sum(mask), clip_grad_norm_, RMSprop
 #include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include <mutex>
@@ -23,6 +24,7 @@
 
 #include "learner_gemms.hpp"
 #include "gru_kernels.hpp"
+#include "gru_fwd_fused.hpp"
 #include "mix_kernels.hpp"
 #include "optim_kernels.hpp"
 
@@ -77,6 +79,7 @@ struct mq_handle {
   bool have_fb = false;
   Dims last;
   int nsplit_fc1 = 1, nsplit_mix = 1, nblk_bwd = 1, nblk_mix = 1, n_norm_part = 0;
+  bool force_unfused = getenv("MQ_UNFUSED_FWD") != nullptr;   // A/B switch for the fused agent forward
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
   int slots = 0;
@@ -339,29 +342,37 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   PhaseTimer pt{h, s};
   const mq_config& c = h->cfg;
 
-  pt.begin(PH_FC1);
-  {
-    Fc1Prob p{d, rp, h->on, h->tg, h->off[MQ_P_FC1_W], h->off[MQ_P_FC1_B], w.X1, w.XIN, RT};
-    MQ_HIP(launch_gemm(p, (int)RT, mq::H, 2, s));
-  }
-  pt.begin(PH_GI);
-  {
-    GiProb p{w.X1, h->on, h->tg, h->off[MQ_P_RNN_W_IH], h->off[MQ_P_RNN_B_IH], w.GI, RT};
-    MQ_HIP(launch_gemm(p, (int)RT, mq::G3, 2, s));
-  }
-  pt.begin(PH_GRUF);
-  {
-    const int rw = pick_rw(d.R, 512);
-    hipError_t e = rw == 1 ? launch_gru_fwd<1>(d, h, L, w, s)
-                 : rw == 2 ? launch_gru_fwd<2>(d, h, L, w, s)
-                 : rw == 4 ? launch_gru_fwd<4>(d, h, L, w, s)
-                           : launch_gru_fwd<8>(d, h, L, w, s);
-    MQ_HIP(e);
-  }
-  pt.begin(PH_FC2);
-  {
-    Fc2Prob p{w.Hs, h->on, h->tg, h->off[MQ_P_FC2_W], h->off[MQ_P_FC2_B], w.Q, RT, d.A};
-    MQ_HIP(launch_gemm(p, (int)RT, d.A, 2, s));
+  const int rw_fwd = pick_rw(d.R, 512);
+  if (rw_fwd == 1 && fused_fwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused) {
+    // one row per workgroup: fc1 / W_ih / fc2 ride on the recurrence's idle matrix cores (gru_fwd_fused.hpp)
+    pt.begin(PH_GRUF);
+    hipLaunchKernelGGL(gru_fwd_fused_kernel<0>, dim3(d.R, 2), dim3(512), 0, s, d, rp, (const float*)h->on,
+                       (const float*)h->tg, L, w);
+    MQ_HIP(hipGetLastError());
+  } else {
+    pt.begin(PH_FC1);
+    {
+      Fc1Prob p{d, rp, h->on, h->tg, h->off[MQ_P_FC1_W], h->off[MQ_P_FC1_B], w.X1, w.XIN, RT};
+      MQ_HIP(launch_gemm(p, (int)RT, mq::H, 2, s));
+    }
+    pt.begin(PH_GI);
+    {
+      GiProb p{w.X1, h->on, h->tg, h->off[MQ_P_RNN_W_IH], h->off[MQ_P_RNN_B_IH], w.GI, RT};
+      MQ_HIP(launch_gemm(p, (int)RT, mq::G3, 2, s));
+    }
+    pt.begin(PH_GRUF);
+    {
+      hipError_t e = rw_fwd == 1 ? launch_gru_fwd<1>(d, h, L, w, s)
+                   : rw_fwd == 2 ? launch_gru_fwd<2>(d, h, L, w, s)
+                   : rw_fwd == 4 ? launch_gru_fwd<4>(d, h, L, w, s)
+                                 : launch_gru_fwd<8>(d, h, L, w, s);
+      MQ_HIP(e);
+    }
+    pt.begin(PH_FC2);
+    {
+      Fc2Prob p{w.Hs, h->on, h->tg, h->off[MQ_P_FC2_W], h->off[MQ_P_FC2_B], w.Q, RT, d.A};
+      MQ_HIP(launch_gemm(p, (int)RT, d.A, 2, s));
+    }
   }
   if (c.mixer == MQ_MIXER_QMIX) {
     pt.begin(PH_HYP);
@@ -481,6 +492,7 @@ int mq_copy_intermediate(mq_handle* h, int which, float* dst, int64_t* count, vo
     case 0: src = h->w.Q; cnt = RT * d.A; break;
     case 1: src = h->w.Q + RT * d.A; cnt = RT * d.A; break;
     case 2: src = h->w.dch; cnt = (int64_t)d.T * d.R; break;
+    case 3: src = h->w.X1; cnt = RT * mq::H; break;
     default: return set_err(MQ_ERR_ARG, "unknown intermediate id");
   }
   if (count) *count = cnt;

@@ -292,7 +292,8 @@ class QLearner:
         return a.permute(1, 0, 2).long()
 
     def last_intermediate(self, which):
-        """0 / 1: online / target mac_out as (B, T+1, n, A); 2: dLoss_num/dchosen as (B, T, n)."""
+        """0 / 1: online / target mac_out as (B, T+1, n, A); 2: dLoss_num/dchosen as (B, T, n);
+        3: online relu(fc1(inputs)) as (B, T+1, n, 64)."""
         B, Tp = self._last_batch
         n, A = self.args.n_agents, self.args.n_actions
         cnt = ctypes.c_int64()
@@ -302,6 +303,8 @@ class QLearner:
         _lib.check(h.lib.mq_copy_intermediate(h.h, which, _lib.ptr(out), ctypes.byref(cnt), _lib.stream_ptr()))
         if which in (0, 1):
             return out.view(Tp, B, n, A).permute(1, 0, 2, 3)
+        if which == 3:
+            return out.view(Tp, B, n, -1).permute(1, 0, 2, 3)
         return out.view(Tp - 1, B, n).permute(1, 0, 2)
 
     def set_timing(self, slots=1, phases=None):

@@ -3,7 +3,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
-#include "../pymarl_amd/csrc/gru_kernels.hpp"
+#include "../pymarl_amd/csrc/gru_fwd_fused.hpp"
 using namespace mq;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
@@ -80,6 +80,45 @@ int main(int argc, char** argv) {
     size_t dyn = (2 * A * 64 + A) * 4;
     return time_it([&] { hipLaunchKernelGGL(kern, dim3((d.R + rw - 1) / rw), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn); });
   };
+  {  // fused agent forward (fc1 / W_ih / fc2 on MFMA inside the recurrence)
+    float* obs = dev_rand((int64_t)B * (T + 1) * n * O, 1.0f);
+    std::vector<int64_t> fl((int64_t)B * (T + 1), 1);
+    int64_t* dfl; CK(hipMalloc(&dfl, fl.size() * 8)); CK(hipMemcpy(dfl, fl.data(), fl.size() * 8, hipMemcpyHostToDevice));
+    Rep rf = rp; rf.obs = obs; rf.filled = dfl;
+    CK(hipMalloc(&w.XIN, RT * d.I * 4));
+    auto runf = [&](auto kern) {
+      return time_it([&] { hipLaunchKernelGGL(kern, dim3(d.R, 2), dim3(512), 0, 0, d, rf, (const float*)P0, (const float*)P1, L, w); });
+    };
+    printf("fused fwd %.1f us\n", runf(gru_fwd_fused_kernel<0>));
+    printf("fused fwd V1(no Hs/Gates st) %.1f us\n", runf(gru_fwd_fused_kernel<1>));
+    printf("fused fwd V4(no chunk pipeline) %.1f us\n", runf(gru_fwd_fused_kernel<4>));
+    printf("fused fwd V5 %.1f us\n", runf(gru_fwd_fused_kernel<5>));
+    runf(gru_fwd_fused_kernel<2>);
+    std::vector<uint64_t> st(2 * 2 * d.R);
+    CK(hipMemcpy(st.data(), w.slab_mix, st.size() * 8, hipMemcpyDeviceToHost));
+    double cyc = 0, tick = 0;
+    for (int i = 0; i < 2 * d.R; ++i) { cyc += st[2 * i]; tick += st[2 * i + 1]; }
+    cyc /= 2 * d.R; tick /= 2 * d.R;
+    printf("fused fwd stamped: %.0f cycles/step, %.3f us/step\n", cyc / d.Tp, tick / 100.0 / d.Tp);
+    runf(gru_fwd_fused_kernel<6>);
+    CK(hipMemcpy(st.data(), w.slab_mix, st.size() * 8, hipMemcpyDeviceToHost));
+    cyc = 0; for (int i = 0; i < 2 * d.R; ++i) cyc += st[2 * i];
+    printf("fused fwd V4 stamped: %.0f cycles/step\n", cyc / (2 * d.R) / d.Tp);
+    for (int var : {8, 12}) {
+      CK(hipFree(w.slab_mix)); CK(hipMalloc(&w.slab_mix, 16 * 8 * 2 * d.R));
+      if (var == 8) runf(gru_fwd_fused_kernel<8>); else runf(gru_fwd_fused_kernel<12>);
+      std::vector<uint64_t> sb(16 * 2 * d.R);
+      CK(hipMemcpy(sb.data(), w.slab_mix, sb.size() * 8, hipMemcpyDeviceToHost));
+      printf("fused V%d cycles per step by phase p:", var);
+      const int nch = (d.Tp + 15) / 16;
+      for (int p = 0; p < 16; ++p) {
+        double c = 0; for (int i = 0; i < 2 * d.R; ++i) c += sb[16 * i + p];
+        const int cnt = nch - (p >= d.Tp - 16 * (nch - 1) ? 1 : 0);
+        printf(" %.0f", c / (2 * d.R) / cnt);
+      }
+      printf("\n");
+    }
+  }
   printf("bwd RW1 %.1f us\n", runb(gru_bwd_kernel<1, 0>, 1));
   printf("bwd RW1 V4(cached inputs) %.1f us\n", runb(gru_bwd_kernel<1, 4>, 1));
   printf("bwd RW1 V8(no accumulate) %.1f us\n", runb(gru_bwd_kernel<1, 8>, 1));
