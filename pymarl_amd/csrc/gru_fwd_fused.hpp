@@ -5,8 +5,8 @@
 // The recurrence is VALU-issue bound (W_hh in VGPRs, DPP quad reductions, one LDS barrier per step) and leaves the
 // matrix cores idle, so the row-parallel contractions around it run on MFMA in the same workgroup, 16 steps at a
 // time (the MFMA M dimension is time). 512 threads, two wave roles meeting at the one barrier per step:
-//  * recurrence waves (0-3, s_setprio 2): the h chain exactly as gru_fwd_body<1>, but with the step's input gates
-//    read from LDS (no global loads at all: nothing for vmcnt to serialise on);
+//  * recurrence waves (0-3): the h chain as gru_fwd_body<1>, but with the step's input gates read from LDS (no
+//    global loads at all: nothing for vmcnt to serialise on) and h kept as a 16-step history (fc2's operand);
 //  * producer waves (4-7): per chunk c of the T loop (p = t & 15), for chunk c+1 and c-1
 //      p = 0        fc2 of chunk c-1: Q[16][A] = H[16][64] W2^T + b2   (hidden-state history in LDS)
 //      p = 1        issue chunk c+1's obs gather (registers; consumed 4 steps later)
@@ -45,8 +45,8 @@ inline bool fused_fwd_ok(int I, int O, int A, int n, int64_t RT) {
 }
 
 struct FusedLds {
-  float hbuf[2][H];
-  float hs[2][FCH][H + 4];   // h history of the last two chunks (fc2 operand)
+  float h0[H];               // init_hidden: zeros (the h_{t-1} of step 0)
+  float hs[2][FCH][H + 4];   // h of the last two chunks: the recurrence's h_{t-1} and fc2's operand
   float gi[2][FCH][G3];      // input gates of the current / next chunk
   float xin[FCH][FXP];       // agent inputs of the next chunk, zero-padded to 4 * Kq
   float x1[FCH][H + 4];
@@ -56,7 +56,8 @@ struct FusedLds {
 };
 
 // VAR: ablation bits for scripts/rec_micro.hip only (production = 0): 1 skip Hs/Gates stores, 2 stamp the T loop,
-// 4 producers idle (recurrence alone on stale gates), 8 per-phase cycle bins.
+// 4 producers idle (recurrence alone on stale gates), 8 per-phase cycle bins, 16 no obs loads, 32 no X1/XIN stores,
+// 64 prologue milestone stamps.
 template <int VAR = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void gru_fwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P0,
                                                                const float* __restrict__ P1, Lay L, Work w) {
@@ -70,17 +71,35 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const int cl = (Tp - 1) / FCH;   // last chunk
   const int r = blockIdx.x;
 
-  // ---- shared prologue: weights to LDS, zero padding, h0
-  for (int e = tid; e < H * FXP; e += 512) {
-    const int nn = e / FXP, k = e - nn * FXP;
-    S.w1[nn][k] = k < I ? P[L.o[MQ_P_FC1_W] + (int64_t)nn * I + k] : 0.0f;
-  }
-  for (int e = tid; e < 16 * (H + 4); e += 512) {
-    const int a = e / (H + 4), k = e - a * (H + 4);
-    S.w2[a][k] = (a < A && k < H) ? P[L.o[MQ_P_FC2_W] + (int64_t)a * H + k] : 0.0f;
+  // ---- shared prologue: weights to LDS (all loads in flight before the first store), zero padding, h0
+  if ((VAR & 64) && tid == 256)
+    ((uint64_t*)w.slab_mix)[16 * (blockIdx.y * gridDim.x + blockIdx.x)] = __builtin_amdgcn_s_memrealtime();
+  {
+    constexpr int N1 = (H * FXP + 511) / 512, N2 = (16 * (H + 4) + 511) / 512;
+    float v1[N1], v2[N2];
+#pragma unroll
+    for (int u = 0; u < N1; ++u) {
+      const int e = tid + 512 * u, nn = e / FXP, k = e - nn * FXP;
+      v1[u] = (e < H * FXP && k < I) ? P[L.o[MQ_P_FC1_W] + (int64_t)nn * I + k] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < N2; ++u) {
+      const int e = tid + 512 * u, a = e / (H + 4), k = e - a * (H + 4);
+      v2[u] = (e < 16 * (H + 4) && a < A && k < H) ? P[L.o[MQ_P_FC2_W] + (int64_t)a * H + k] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < N1; ++u) {
+      const int e = tid + 512 * u;
+      if (e < H * FXP) (&S.w1[0][0])[e] = v1[u];
+    }
+#pragma unroll
+    for (int u = 0; u < N2; ++u) {
+      const int e = tid + 512 * u;
+      if (e < 16 * (H + 4)) (&S.w2[0][0])[e] = v2[u];
+    }
   }
   for (int e = tid; e < FCH * FXP; e += 512) (&S.xin[0][0])[e] = 0.0f;
-  if (tid < H) S.hbuf[0][tid] = 0.0f;   // init_hidden: h0 = 0
+  if (tid < H) S.h0[tid] = 0.0f;   // init_hidden: h0 = 0
 
   if (rec) {
     // ================================================================ recurrence waves
@@ -99,13 +118,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                 bhn = P[L.o[MQ_P_RNN_B_HH] + 2 * H + j];
     drain_vmem();
     for (int i = 0; i < 5; ++i) lds_barrier();   // the producers' chunk-0 prologue (5 barriers)
-    __builtin_amdgcn_s_setprio(2);
     float* Hz = w.Hs;   // online only: the backward pass reads h_{t-1}
     const int gcol = min(q, 2) * H + j;
     float own = S.gi[0][0][gcol];   // this step's input gate, read right after the previous step's barrier
     auto step = [&](int t) {
       const int p = t & (FCH - 1), c = t / FCH;
-      const float* hb = S.hbuf[t & 1];
+      const float* hb = t == 0 ? S.h0 : S.hs[((t - 1) / FCH) & 1][(t - 1) & (FCH - 1)];
       float sr, sz, sn;
       {
         const f32x4* hv4 = (const f32x4*)(&hb[16 * q]);
@@ -133,8 +151,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const float ng = quad_bcast<2>(tanh_fast(own + ghn * rg));
       const float hp = hb[j];
       const float h1 = (hp - ng) * zg + ng;   // ATen gru_cell: (hx - n) * z + n
-      if (q == 0) S.hbuf[(t + 1) & 1][j] = h1;
-      if (q == 1) S.hs[c & 1][p][j] = h1;
+      if (q == 0) S.hs[c & 1][p][j] = h1;
       if (online && !(VAR & 1)) {
         const int64_t tr = (int64_t)t * R + r;
         if (q == 0) Hz[tr * H + j] = h1;
@@ -166,7 +183,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     } else {
       for (int t = 0; t < Tp; ++t) step(t);
     }
-    __builtin_amdgcn_s_setprio(0);
     if ((VAR & 2) && tid == 0) {   // diagnostic only: shader cycles and 100 MHz ticks of the whole T loop
       const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
       ((uint64_t*)w.slab_mix)[2 * (blockIdx.y * gridDim.x + blockIdx.x)] = c1 - c0;
@@ -216,7 +232,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const float* base = obs_row + (int64_t)t0 * nO;
     const int lim = (Tp - 1 - t0) * nO + O - 1;   // last valid element offset of this chunk
 #pragma unroll
-    for (int s = 0; s < FGATHER; ++s) xr[s] = base[min(opaque(gsl[s]) & 0xFFFF, lim)];
+    for (int s = 0; s < FGATHER; ++s) xr[s] = (VAR & 16) ? (float)s : base[min(opaque(gsl[s]) & 0xFFFF, lim)];
     {
       const int t = min(max(t0 + (ptid & (FCH - 1)), 1), Tp - 1) - 1;
       f_ld = *(const int*)(rp.filled + slot0 + t);
@@ -233,7 +249,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const int i = gs >> 16, col = (gs & 0xFFFF) - i * nO;
       const bool ok = t0 + i < Tp;
       S.xin[i][col] = ok ? xr[s] : 0.0f;
-      if (online && ok) xg[i * R * I + col] = xr[s];   // RT * I < 2^31 (host check)
+      if (online && ok && !(VAR & 32)) xg[i * R * I + col] = xr[s];   // RT * I < 2^31 (host check)
     }
     // actions_onehot[t-1] is zero unless slot t-1 was filled (runner contract)
     if (ptid < FCH) {
@@ -248,7 +264,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       if (d.last_action && col < A) v = col == S.aprev[i] ? 1.0f : 0.0f;
       else v = (col - (d.last_action ? A : 0)) == ag ? 1.0f : 0.0f;
       S.xin[i][O + col] = v;
-      if (online && t < Tp) XINo[((int64_t)t * R + r) * I + O + col] = v;
+      if (online && t < Tp && !(VAR & 32)) XINo[((int64_t)t * R + r) * I + O + col] = v;
     }
   };
   f32x4 acc1 = {0, 0, 0, 0}, acc1b = {0, 0, 0, 0}, accg[3] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -271,7 +287,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const int i = 4 * g + e, t = t0 + i;
       const float x = fmaxf((acc1[e] + acc1b[e]) + b1, 0.0f);
       S.x1[i][16 * wv + c16] = x;
-      if (online && t < Tp) X1o[((int64_t)t * R + r) * H + 16 * wv + c16] = x;
+      if (online && t < Tp && !(VAR & 32)) X1o[((int64_t)t * R + r) * H + 16 * wv + c16] = x;
     }
     acc1 = f32x4{0, 0, 0, 0};
     acc1b = f32x4{0, 0, 0, 0};
@@ -316,19 +332,29 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   };
 
   // chunk 0 synchronously (5 barriers, matched by the recurrence waves)
+  uint64_t* stp = (uint64_t*)w.slab_mix + 16 * (blockIdx.y * gridDim.x + blockIdx.x);
+  auto stamp = [&](int k) {   // VAR bit 64 (microbenchmark): prologue milestones, 100 MHz ticks
+    if ((VAR & 64) && ptid == 0) stp[k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(1);
   issue_gather(0);
   drain_vmem();
+  stamp(2);
   lds_barrier();   // 1: weights, padding staged
+  stamp(3);
   store_gather(0);
   lds_barrier();   // 2
   onehots(0);
   lds_barrier();   // 3
+  stamp(4);
   fc1_part(0, FKQ / 4);
   fc1_epi(0);
   lds_barrier();   // 4
+  stamp(5);
   gi_part(0, 16);
   gi_epi(0);
   lds_barrier();   // 5
+  stamp(6);
 
   if (!(VAR & 4)) {
     for (int c = 0; c <= cl; ++c) {
@@ -361,6 +387,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   } else {
     for (int t = 0; t < Tp; ++t) lds_barrier();
   }
+  stamp(7);
   // the last chunk (and the previous one's store when the last chunk is a single step) after the final barrier,
   // in wave 0 alone
   if (cl >= 1 && Tp - FCH * cl < 2) fc2_store(cl - 1);
@@ -382,6 +409,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       if (t < Tp && c16 < A) Qz[((int64_t)t * R + r) * A + c16] = (q0[e] + q1[e]) + b2;
     }
   }
+  stamp(8);
 }
 
 }  // namespace mq

@@ -1,5 +1,6 @@
 // Microbenchmark of the persistent GRU recurrence kernels at a given (B, n, T) with random data.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/rec_micro.hip -o /tmp/rec_micro && /tmp/rec_micro 32 8 120
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -104,9 +105,26 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(st.data(), w.slab_mix, st.size() * 8, hipMemcpyDeviceToHost));
     cyc = 0; for (int i = 0; i < 2 * d.R; ++i) cyc += st[2 * i];
     printf("fused fwd V4 stamped: %.0f cycles/step\n", cyc / (2 * d.R) / d.Tp);
+    {
+      CK(hipFree(w.slab_mix)); CK(hipMalloc(&w.slab_mix, 16 * 8 * 2 * d.R));
+      runf(gru_fwd_fused_kernel<64>);
+      std::vector<uint64_t> sb(16 * 2 * d.R);
+      CK(hipMemcpy(sb.data(), w.slab_mix, sb.size() * 8, hipMemcpyDeviceToHost));
+      uint64_t t0 = ~0ull;
+      for (int i = 0; i < 2 * d.R; ++i) t0 = std::min(t0, sb[16 * i]);
+      printf("fused prologue milestones (us after the earliest WG start, mean / max over WGs):");
+      for (int k = 0; k <= 8; ++k) {
+        double m = 0, mx = 0;
+        for (int i = 0; i < 2 * d.R; ++i) { double v = (sb[16 * i + k] - t0) / 100.0; m += v; mx = std::max(mx, v); }
+        printf(" [%d] %.2f/%.2f", k, m / (2 * d.R), mx);
+      }
+      printf("\n");
+    }
     for (int var : {8, 12}) {
       CK(hipFree(w.slab_mix)); CK(hipMalloc(&w.slab_mix, 16 * 8 * 2 * d.R));
-      if (var == 8) runf(gru_fwd_fused_kernel<8>); else runf(gru_fwd_fused_kernel<12>);
+      if (var == 8) runf(gru_fwd_fused_kernel<8>);
+      else runf(gru_fwd_fused_kernel<12>);
+
       std::vector<uint64_t> sb(16 * 2 * d.R);
       CK(hipMemcpy(sb.data(), w.slab_mix, sb.size() * 8, hipMemcpyDeviceToHost));
       printf("fused V%d cycles per step by phase p:", var);
