@@ -1,0 +1,335 @@
+// Fused backward for one-row workgroups: BPTT of the online agent (q_learner.py:100-101 through rnn_agent.py:24-28)
+// with every weight-gradient contraction and the fc1 input gradient on MFMA beside the VALU chain.
+//
+// 512 threads, two wave roles meeting at one barrier per step (T loop runs backwards):
+//  * chain waves (0-3): the serial part, as gru_bwd_kernel<1>: gate derivatives from dh (lane-split), the
+//    W_hh^T mat-vec, the carry. Each step's [dgh | h_{t-1}] and dgi land in a 16-step LDS history instead of
+//    HBM (no dGI round trip);
+//  * producer waves (4-7): the fc2 grads of the step (VALU, as before) and, for the last complete 16-step chunk
+//    C while the chain walks chunk C-1 (u = 16(C-1) + 15 - t):
+//      u = 0         issue C's X1 / XIN row loads (written by the forward)
+//      u = 1 .. 4    dW_hh += dGH^T H_prev   [192 x 64, K = 16 steps]      12 MFMA / step
+//      u = 4         stage X1 / XIN in LDS
+//      u = 5 .. 8    dW_ih += dGI^T X1       [192 x 64, K = 16]            12 MFMA / step
+//      u = 9 .. 12   dX1 = (dGI W_ih) o relu'(X1)   [16 x 64, K = 192]     12 MFMA / step (W_ih in LDS)
+//      u = 13 .. 15  dW1 += dX1^T XIN        [64 x I, K = 16]              7 / 7 / 14 MFMA
+//    and chunk 0 after the chain finishes. dW_hh / dW_ih / dW1 accumulate in the MFMA C layout for the whole T
+//    loop (48 + 48 + 28 VGPRs), so the Dx1 / Dw1 GEMMs and the dGI / dX1 buffers of the unfused path disappear.
+// Writes the per-workgroup slabs [w_ih | w_hh | b_ih | b_hh | fc2.w | fc2.b] and [fc1.w | fc1.b].
+//
+// MFMA maps as gru_fwd_fused.hpp (v_mfma_f32_16x16x4_f32: A[i = c][kk = g], B[kk = g][j = c], D[4g + r][c]).
+#pragma once
+#include "gru_fwd_fused.hpp"
+
+namespace mq {
+
+constexpr int BRP = 4 * H + 4;   // history row pitch: [dgh | h_{t-1}] and [dgi | -], padded against bank conflicts
+
+struct BwdFusedLds {
+  float gh[2][FCH][BRP];     // per step: dgh (3H) | h_{t-1} (H), chunk-double-buffered
+  float gi[2][FCH][BRP];     // per step: dgi (3H) | unused
+  float x1[FCH][H + 4];      // X1 of the chunk being reduced
+  float xin[FCH][FXP];       // XIN of the chunk being reduced (zero-padded to 4 * Kq)
+  float dx1[FCH][H + 4];     // dX1 of the chunk being reduced
+  float db1[4][H];           // fc1 bias-grad partials of the four lane groups
+  float wih[G3][H + 1];      // W_ih (dX1's B operand); odd pitch: the four lane groups read rows 48 apart
+  float dch[2];              // this step's dLoss/dchosen (0 at t = T) and action, for the fc2 grads
+  int act[2];
+};
+
+inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_fwd_ok(I, O, A, n, RT); }
+
+// VAR: ablation bits for scripts/rec_micro.hip only (production = 0): 4 producers do no MFMA work.
+template <int VAR = 0>
+__global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
+                                                            Work w, int64_t slab_len, int64_t slab1_len) {
+  __shared__ BwdFusedLds S;
+  extern __shared__ float dyn[];   // W2 [A][H] | dW2 partial [A][H] | db2 [A]
+  const int tid = threadIdx.x;
+  const bool chain = tid < 256;
+  const int lt = tid & 255, k = lt >> 2, q = lt & 3;
+  const int R = d.R, A = d.A, T = d.T, Tp = d.Tp, I = d.I;
+  const int cl = (Tp - 1) / FCH;
+  const int r = blockIdx.x;
+  float* w2_s = dyn;
+  float* dw2_s = dyn + A * H;
+  float* db2_s = dyn + 2 * A * H;
+
+  for (int i = tid; i < A * H; i += 512) { w2_s[i] = P[L.o[MQ_P_FC2_W] + i]; dw2_s[i] = 0.0f; }
+  for (int i = tid; i < A; i += 512) db2_s[i] = 0.0f;
+  // zero the history rows past Tp of the top (partial) chunk and the XIN padding
+  for (int e = tid; e < 2 * FCH * BRP; e += 512) { (&S.gh[0][0][0])[e] = 0.0f; (&S.gi[0][0][0])[e] = 0.0f; }
+  for (int e = tid; e < FCH * FXP; e += 512) (&S.xin[0][0])[e] = 0.0f;
+  {
+    constexpr int NW = G3 * H / 512;   // W_ih to LDS, all loads in flight first
+    float v[NW];
+#pragma unroll
+    for (int u = 0; u < NW; ++u) v[u] = P[L.o[MQ_P_RNN_W_IH] + tid + 512 * u];
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      const int e = tid + 512 * u, m = e / H;
+      S.wih[m][e - m * H] = v[u];
+    }
+  }
+
+  const int b = (int)fdiv((uint32_t)r, d.dN), ag = r - b * d.n;
+  const int64_t* arow = rp.actions + rp.ep(b) * d.t_stride * d.n + ag;   // &actions[ep(b)][0][agent]
+  const int64_t base = L.o[MQ_P_RNN_W_IH];
+  float* slab = w.slab_rnn + (int64_t)blockIdx.x * slab_len;
+  const int64_t o_hh = L.o[MQ_P_RNN_W_HH] - base, o_bi = L.o[MQ_P_RNN_B_IH] - base,
+                o_bh = L.o[MQ_P_RNN_B_HH] - base, o_w2 = L.o[MQ_P_FC2_W] - base, o_b2 = L.o[MQ_P_FC2_B] - base;
+
+  if (chain) {
+    // ================================================================ chain waves
+    float wT[48];   // W_hh[48q .. 48q+47][k]
+    {
+      const float* Whh = P + L.o[MQ_P_RNN_W_HH];
+#pragma unroll
+      for (int c = 0; c < 48; ++c) wT[c] = Whh[(48 * q + c) * H + k];
+    }
+    // lane-split inputs of a step: lane q loads gate component q and one of (h_{t-1}, -, dch, action)
+    struct In { float g, aux; };
+    auto load = [&](int t, In& s) {
+      const int tc = max(t, 0), td = min(tc, T - 1);
+      const int64_t tr = (int64_t)tc * R + r;
+      const float* src = q == 0   ? w.Hs + (tc > 0 ? tr - R : tr) * H + k
+                         : q == 3 ? (const float*)(arow + (int64_t)tc * d.n)
+                                  : w.dch + (int64_t)td * R + r;
+      s.g = w.Gates[tr * (4 * H) + q * H + k];
+      s.aux = *src;
+    };
+    float carry = 0.0f, db_i = 0.0f, db_h = 0.0f;   // bias grads: this lane's component q of b_ih / b_hh
+    auto step = [&](int t, const In& cur, In& nxt) {
+      load(t - 1, nxt);   // previous (earlier) step's inputs, in flight under this step
+      const int p = t & (FCH - 1), cb = (t / FCH) & 1, pb = t & 1;
+      const bool live = t < Tp;
+      const float gr = quad_bcast<0>(cur.g), gz = quad_bcast<1>(cur.g), gn = quad_bcast<2>(cur.g),
+                  ghn = quad_bcast<3>(cur.g);
+      const float hp = t > 0 ? quad_bcast<0>(cur.aux) : 0.0f;
+      const float dchv = (live && t < T) ? quad_bcast<2>(cur.aux) : 0.0f;
+      const int a = __builtin_bit_cast(int, quad_bcast<3>(cur.aux));
+      const float dh = carry + dchv * w2_s[a * H + k];
+      if (k == 0 && q == 0) { S.dch[pb] = dchv; S.act[pb] = a; }
+      const float dn = dh * (1.0f - gz);
+      const float dz = dh * (hp - gn);
+      const float dan = dn * (1.0f - gn * gn);
+      const float dar = (dan * ghn) * (gr * (1.0f - gr));
+      const float daz = dz * (gz * (1.0f - gz));
+      const float mine_i = q == 0 ? dar : (q == 1 ? daz : dan);   // dgi component q
+      const float mine_h = q == 2 ? dan * gr : mine_i;             // dgh component q
+      S.gh[cb][p][q * H + k] = q < 3 ? mine_h : hp;
+      S.gi[cb][p][q * H + k] = mine_i;
+      db_i += q < 3 ? mine_i : 0.0f;
+      db_h += q < 3 ? mine_h : 0.0f;
+      const float cz = dh * gz;
+      lds_barrier();
+      // dh_{t-1} = dh * z + W_hh^T dgh
+      const f32x4* dg4 = (const f32x4*)(&S.gh[cb][p][48 * q]);
+      float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+#pragma unroll
+      for (int c4 = 0; c4 < 12; ++c4) {
+        const f32x4 dg = dg4[c4];
+        const int c = 4 * c4;
+        a0 = fmaf(wT[c], dg[0], a0); a1 = fmaf(wT[c + 1], dg[1], a1);
+        a2 = fmaf(wT[c + 2], dg[2], a2); a3 = fmaf(wT[c + 3], dg[3], a3);
+      }
+      carry = cz + quad_sum((a0 + a1) + (a2 + a3));
+    };
+    In sa, sb;
+    load(Tp - 1, sa);
+    drain_vmem();
+    lds_barrier();
+    int t = Tp - 1;
+    for (; t - 1 >= 0; t -= 2) {
+      step(t, sa, sb);
+      step(t - 1, sb, sa);
+    }
+    if (t >= 0) step(t, sa, sb);
+    lds_barrier();   // producer tail: chunk 0 (2 barriers)
+    lds_barrier();
+    if (q < 3) { slab[o_bi + q * H + k] = db_i; slab[o_bh + q * H + k] = db_h; }
+  } else {
+    // ================================================================== producer waves
+    const int ptid = tid - 256, wv = ptid >> 6, lane = ptid & 63, g = lane >> 4, c16 = lane & 15;
+    const int Kq = (I + 15) / 16 * 4;
+    f32x4 acc_hh[3][4], acc_ih[3][4], acc_w1[7];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) { acc_hh[i][jj] = f32x4{0, 0, 0, 0}; acc_ih[i][jj] = f32x4{0, 0, 0, 0}; }
+#pragma unroll
+    for (int i = 0; i < 7; ++i) acc_w1[i] = f32x4{0, 0, 0, 0};
+    f32x4 dxa = {0, 0, 0, 0}, dxb = {0, 0, 0, 0};
+    float db1p = 0.0f;
+
+    // X1 / XIN rows of a chunk: slot s of this thread covers element ptid + 256 s of [16][H] and of [16][I]
+    constexpr int NX1 = FCH * H / 256, NXI = (FCH * 4 * FKQ + 255) / 256;
+    float rx1[NX1], rxi[NXI];
+    auto issue_rows = [&](int C) {
+      const int t0 = FCH * C;
+#pragma unroll
+      for (int s = 0; s < NX1; ++s) {
+        const int e = ptid + 256 * s, i = e / H, col = e - i * H, t = min(t0 + i, Tp - 1);
+        rx1[s] = w.X1[((int64_t)t * R + r) * H + col];
+      }
+#pragma unroll
+      for (int s = 0; s < NXI; ++s) {
+        const int e = opaque(ptid + 256 * s), i = e / I, col = e - i * I, t = min(t0 + i, Tp - 1);
+        rxi[s] = e < FCH * I ? w.XIN[((int64_t)t * R + r) * I + col] : 0.0f;
+      }
+    };
+    auto store_rows = [&](int C) {
+      const int t0 = FCH * C;
+#pragma unroll
+      for (int s = 0; s < NX1; ++s) {
+        const int e = ptid + 256 * s, i = e / H, col = e - i * H;
+        S.x1[i][col] = t0 + i < Tp ? rx1[s] : 0.0f;
+      }
+#pragma unroll
+      for (int s = 0; s < NXI; ++s) {
+        const int e = opaque(ptid + 256 * s), i = e / I, col = e - i * I;
+        if (e < FCH * I) S.xin[i][col] = t0 + i < Tp ? rxi[s] : 0.0f;
+      }
+    };
+    // dW_hh / dW_ih: wave wv owns M-tiles 3wv .. 3wv+2 (gate rows) x all 4 N-tiles; K = 16 steps, kk = 4 kb + g
+    auto dw_rec = [&](int C, int kb0, int kb1, bool ih) {
+      const int cb = C & 1;
+#pragma unroll
+      for (int kb = kb0; kb < kb1; ++kb) {
+        const int row = 4 * kb + g;
+        float av[3], bv[4];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) av[i] = (ih ? S.gi : S.gh)[cb][row][16 * (3 * wv + i) + c16];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) bv[jj] = ih ? S.x1[row][16 * jj + c16] : S.gh[cb][row][3 * H + 16 * jj + c16];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            if (ih) acc_ih[i][jj] = mfma16x4(av[i], bv[jj], acc_ih[i][jj]);
+            else acc_hh[i][jj] = mfma16x4(av[i], bv[jj], acc_hh[i][jj]);
+          }
+      }
+    };
+    // dX1[16][64] = dGI[16][192] W_ih[192][64]: wave wv owns N-tile wv; lane group g owns k in [48 g, 48 g + 48)
+    auto dx1_part = [&](int C, int m0, int m1) {   // b128 groups [m0, m1) of 12
+      const int cb = C & 1;
+#pragma unroll
+      for (int m = m0; m < m1; ++m) {
+        const f32x4 av = *(const f32x4*)&S.gi[cb][c16][48 * g + 4 * m];
+        const float* wb = &S.wih[48 * g + 4 * m][16 * wv + c16];
+        dxa = mfma16x4(av[0], wb[0], dxa);
+        dxb = mfma16x4(av[1], wb[H + 1], dxb);
+        dxa = mfma16x4(av[2], wb[2 * (H + 1)], dxa);
+        dxb = mfma16x4(av[3], wb[3 * (H + 1)], dxb);
+      }
+    };
+    auto dx1_epi = [&]() {   // relu'(X1) mask, fc1 bias-grad partial
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * g + e, col = 16 * wv + c16;
+        const float v = S.x1[i][col] > 0.0f ? dxa[e] + dxb[e] : 0.0f;
+        S.dx1[i][col] = v;
+        db1p += v;
+      }
+      dxa = f32x4{0, 0, 0, 0};
+      dxb = f32x4{0, 0, 0, 0};
+    };
+    // dW1[64][I] += dX1^T XIN: wave wv owns M-tile wv (fc1 unit rows) x 7 N-tiles (inputs); kk = 4 kb + g
+    auto dw1_part = [&](int kb0, int kb1) {
+#pragma unroll
+      for (int kb = kb0; kb < kb1; ++kb) {
+        const int row = 4 * kb + g;
+        const float av = S.dx1[row][16 * wv + c16];
+#pragma unroll
+        for (int nt = 0; nt < 7; ++nt) {
+          if (16 * nt >= 4 * Kq) break;
+          acc_w1[nt] = mfma16x4(av, S.xin[row][16 * nt + c16], acc_w1[nt]);
+        }
+      }
+    };
+    // fc2 grads of step t: dW2[a][k] += dchosen * h_t[k]; (a, k) owned by lane (k, q = a % 4); h_t was the
+    // h_{t-1} record of step t+1
+    float h_next = 0.0f;
+    auto fc2_grads = [&](int t) {
+      const int pb = t & 1, p = t & (FCH - 1), cb = (t / FCH) & 1;
+      if (t < T) {
+        const int a = S.act[pb];
+        if ((a & 3) == q) {
+          const float dchv = S.dch[pb];
+          dw2_s[a * H + k] += dchv * h_next;
+          if (k == 0) db2_s[a] += dchv;
+        }
+      }
+      h_next = S.gh[cb][p][3 * H + k];
+    };
+
+    lds_barrier();
+    for (int c = cl; c >= 0; --c) {
+      const int C = c + 1;
+      const bool work = !(VAR & 4) && C <= cl;
+#pragma unroll
+      for (int u = 0; u < FCH; ++u) {
+        const int t = FCH * c + FCH - 1 - u;
+        if (t >= Tp) continue;
+        lds_barrier();   // step t's records published
+        fc2_grads(t);
+        if (work) {
+          if (u == 0) issue_rows(C);
+          if (u >= 1 && u <= 4) dw_rec(C, u - 1, u, false);
+          if (u == 4) store_rows(C);
+          if (u >= 5 && u <= 8) dw_rec(C, u - 5, u - 4, true);
+          if (u >= 9 && u <= 12) dx1_part(C, 3 * (u - 9), 3 * (u - 8));
+          if (u == 12) dx1_epi();
+          if (u == 13) dw1_part(0, 1);
+          if (u == 14) dw1_part(1, 2);
+          if (u == 15) dw1_part(2, 4);
+        }
+      }
+    }
+    // tail: chunk 0 (2 barriers, matched by the chain waves)
+    if (!(VAR & 4)) {
+      issue_rows(0);
+      dw_rec(0, 0, 4, false);
+      drain_vmem();
+      store_rows(0);
+    }
+    lds_barrier();
+    if (!(VAR & 4)) {
+      dw_rec(0, 0, 4, true);
+      dx1_part(0, 0, 12);
+      dx1_epi();
+    }
+    lds_barrier();
+    if (!(VAR & 4)) dw1_part(0, 4);
+
+    // per-workgroup slabs in the MFMA C layout: element (16 tile + 4 g + e, 16 tile' + c16)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = 16 * (3 * wv + i) + 4 * g + e, nn = 16 * jj + c16;
+          slab[m * H + nn] = acc_ih[i][jj][e];
+          slab[o_hh + m * H + nn] = acc_hh[i][jj][e];
+        }
+    float* slab1 = w.slab_fc1 + (int64_t)blockIdx.x * slab1_len;
+#pragma unroll
+    for (int nt = 0; nt < 7; ++nt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = 16 * wv + 4 * g + e, nn = 16 * nt + c16;
+        if (nn < I) slab1[m * I + nn] = acc_w1[nt][e];
+      }
+    S.db1[g][16 * wv + c16] = db1p;
+  }
+  lds_barrier();
+  for (int i = tid; i < A * H; i += 512) slab[o_w2 + i] = dw2_s[i];
+  for (int i = tid; i < A; i += 512) slab[o_b2 + i] = db2_s[i];
+  if (tid < H)
+    w.slab_fc1[(int64_t)blockIdx.x * slab1_len + H * I + tid] =
+        (S.db1[0][tid] + S.db1[1][tid]) + (S.db1[2][tid] + S.db1[3][tid]);
+}
+
+}  // namespace mq

@@ -25,6 +25,7 @@
 #include "learner_gemms.hpp"
 #include "gru_kernels.hpp"
 #include "gru_fwd_fused.hpp"
+#include "gru_bwd_fused.hpp"
 #include "mix_kernels.hpp"
 #include "optim_kernels.hpp"
 
@@ -79,7 +80,8 @@ struct mq_handle {
   bool have_fb = false;
   Dims last;
   int nsplit_fc1 = 1, nsplit_mix = 1, nblk_bwd = 1, nblk_mix = 1, n_norm_part = 0;
-  bool force_unfused = getenv("MQ_UNFUSED_FWD") != nullptr;   // A/B switch for the fused agent forward
+  bool force_unfused = getenv("MQ_UNFUSED_FWD") != nullptr;       // A/B switch for the fused agent forward
+  bool force_unfused_bwd = getenv("MQ_UNFUSED_BWD") != nullptr;   // A/B switch for the fused BPTT
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
   int slots = 0;
@@ -253,7 +255,8 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
   const int64_t nmix = (Mm + 3) / 4;
   const int64_t NH = h->NH;
   auto ng = [](int64_t ns) { return std::min<int64_t>(ns, kRedZ); };
-  const int64_t red_tmp = ng(Rm) * h->len_rnn + ng(kNsplitMax) * (Hd * h->I + Hd) + ng(kNsplitMax) * h->len_mix +
+  const int64_t nfc1 = std::max<int64_t>(kNsplitMax, Rm);   // fc1 slabs: split-K GEMM, or one per fused-BPTT row
+  const int64_t red_tmp = ng(Rm) * h->len_rnn + ng(nfc1) * (Hd * h->I + Hd) + ng(kNsplitMax) * h->len_mix +
                           ng(nmix) * (h->E + 1) + ng(nmix) * 8;
   const int64_t norm_parts = (Hd * h->I + Hd + 255) / 256 + (h->len_rnn + 255) / 256 + (h->len_mix + 255) / 256 +
                              (h->E + 1 + 255) / 256 + 1 + 8;
@@ -268,7 +271,7 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
       Mm * n,                                        // dch
       RT * 3 * Hd,                                   // dGI
       RT * Hd,                                       // dP1
-      (int64_t)kNsplitMax * (Hd * h->I + Hd),        // slab_fc1
+      nfc1 * (Hd * h->I + Hd),                       // slab_fc1
       Rm * h->len_rnn,                               // slab_rnn (RW = 1 worst case)
       (int64_t)kNsplitMax * h->len_mix,              // slab_mix
       nmix * (h->E + 1),                             // slab_v2
@@ -385,30 +388,40 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
                      (const float*)h->tg, L, w, curmax);
   MQ_HIP(hipGetLastError());
   pt.begin(PH_GRUB);
-  {
-    // RW >= 4 spills the 96 role registers + per-row prefetch sets at 512 threads; cap at 2
-    const int rw = std::min(2, pick_rw(d.R, 256));
-    hipError_t e = rw == 1 ? launch_gru_bwd<1>(d, rp, h, L, w, s, &h->nblk_bwd)
-                 : rw == 2 ? launch_gru_bwd<2>(d, rp, h, L, w, s, &h->nblk_bwd)
-                           : launch_gru_bwd<4>(d, rp, h, L, w, s, &h->nblk_bwd);
-    MQ_HIP(e);
-  }
-  pt.begin(PH_DX1);
-  {
-    Dx1Prob p{w.dGI, h->on + h->off[MQ_P_RNN_W_IH], w.X1, w.dP1, RT};
-    MQ_HIP(launch_gemm(p, (int)RT, mq::H, 1, s));
-  }
-  pt.begin(PH_DW1);
-  {
-    const int tiles = (d.I + Dw1Prob::BN - 1) / Dw1Prob::BN;
-    int ns = (int)std::min<int64_t>(kNsplitMax, std::max<int64_t>(1, RT / 256));
-    ns = std::max(1, std::min(ns, (512 + tiles - 1) / tiles));
-    // keep every split non-empty under krange_split's GBK rounding
-    int64_t chunk = ((RT + ns - 1) / ns + GBK - 1) / GBK * GBK;
-    ns = (int)((RT + chunk - 1) / chunk);
-    h->nsplit_fc1 = ns;
-    Dw1Prob p{d.I, w.dP1, w.XIN, w.slab_fc1, RT, ns};
-    MQ_HIP(launch_gemm(p, mq::H, d.I, ns, s));
+  const int rw_bwd = std::min(2, pick_rw(d.R, 256));
+  if (rw_bwd == 1 && fused_bwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused_bwd) {
+    // one row per workgroup: dW_hh / dW_ih / dX1 / dW1 on the chain's idle matrix cores (gru_bwd_fused.hpp)
+    h->nblk_bwd = d.R;
+    h->nsplit_fc1 = d.R;
+    const size_t dyn = ((size_t)2 * d.A * mq::H + d.A) * sizeof(float);
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<0>, dim3(d.R), dim3(512), dyn, s, d, rp, (const float*)h->on, L, w,
+                       h->len_rnn, (int64_t)mq::H * d.I + mq::H);
+    MQ_HIP(hipGetLastError());
+  } else {
+    {
+      // RW >= 4 spills the 96 role registers + per-row prefetch sets at 512 threads; cap at 2
+      hipError_t e = rw_bwd == 1 ? launch_gru_bwd<1>(d, rp, h, L, w, s, &h->nblk_bwd)
+                   : rw_bwd == 2 ? launch_gru_bwd<2>(d, rp, h, L, w, s, &h->nblk_bwd)
+                                 : launch_gru_bwd<4>(d, rp, h, L, w, s, &h->nblk_bwd);
+      MQ_HIP(e);
+    }
+    pt.begin(PH_DX1);
+    {
+      Dx1Prob p{w.dGI, h->on + h->off[MQ_P_RNN_W_IH], w.X1, w.dP1, RT};
+      MQ_HIP(launch_gemm(p, (int)RT, mq::H, 1, s));
+    }
+    pt.begin(PH_DW1);
+    {
+      const int tiles = (d.I + Dw1Prob::BN - 1) / Dw1Prob::BN;
+      int ns = (int)std::min<int64_t>(kNsplitMax, std::max<int64_t>(1, RT / 256));
+      ns = std::max(1, std::min(ns, (512 + tiles - 1) / tiles));
+      // keep every split non-empty under krange_split's GBK rounding
+      int64_t chunk = ((RT + ns - 1) / ns + GBK - 1) / GBK * GBK;
+      ns = (int)((RT + chunk - 1) / chunk);
+      h->nsplit_fc1 = ns;
+      Dw1Prob p{d.I, w.dP1, w.XIN, w.slab_fc1, RT, ns};
+      MQ_HIP(launch_gemm(p, mq::H, d.I, ns, s));
+    }
   }
   if (c.mixer == MQ_MIXER_QMIX) {
     pt.begin(PH_DWH);
