@@ -7,8 +7,12 @@
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 namespace mq {
+
+// Two f32 FMAs in one v_pk_fma_f32 (half the issue slots of two v_fma_f32 at the same FLOP rate).
+MQ_DEV f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 constexpr float kNegMask = -9999999.0f;   // q_learner.py:68,74
 

@@ -39,7 +39,8 @@ struct BwdFusedLds {
 
 inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_fwd_ok(I, O, A, n, RT); }
 
-// VAR: ablation bits for scripts/rec_micro.hip only (production = 0): 4 producers do no MFMA work.
+// VAR: ablation bits for scripts/rec_micro.hip only (production = 0): 4 producers do no MFMA work, 8 per-phase
+// cycle bins of the chain.
 template <int VAR = 0>
 __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
                                                             Work w, int64_t slab_len, int64_t slab1_len) {
@@ -81,11 +82,11 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
 
   if (chain) {
     // ================================================================ chain waves
-    float wT[48];   // W_hh[48q .. 48q+47][k]
+    f32x2 wT[24];   // W_hh[48q .. 48q+47][k] as pairs for v_pk_fma_f32
     {
       const float* Whh = P + L.o[MQ_P_RNN_W_HH];
 #pragma unroll
-      for (int c = 0; c < 48; ++c) wT[c] = Whh[(48 * q + c) * H + k];
+      for (int c = 0; c < 24; ++c) wT[c] = f32x2{Whh[(48 * q + 2 * c) * H + k], Whh[(48 * q + 2 * c + 1) * H + k]};
     }
     // lane-split inputs of a step: lane q loads gate component q and one of (h_{t-1}, -, dch, action)
     struct In { float g, aux; };
@@ -125,26 +126,50 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       lds_barrier();
       // dh_{t-1} = dh * z + W_hh^T dgh
       const f32x4* dg4 = (const f32x4*)(&S.gh[cb][p][48 * q]);
-      float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+      f32x2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
 #pragma unroll
       for (int c4 = 0; c4 < 12; ++c4) {
         const f32x4 dg = dg4[c4];
-        const int c = 4 * c4;
-        a0 = fmaf(wT[c], dg[0], a0); a1 = fmaf(wT[c + 1], dg[1], a1);
-        a2 = fmaf(wT[c + 2], dg[2], a2); a3 = fmaf(wT[c + 3], dg[3], a3);
+        a01 = pk_fma(wT[2 * c4], f32x2{dg[0], dg[1]}, a01);
+        a23 = pk_fma(wT[2 * c4 + 1], f32x2{dg[2], dg[3]}, a23);
       }
-      carry = cz + quad_sum((a0 + a1) + (a2 + a3));
+      carry = cz + quad_sum((a01.x + a01.y) + (a23.x + a23.y));
     };
     In sa, sb;
     load(Tp - 1, sa);
     drain_vmem();
     lds_barrier();
     int t = Tp - 1;
-    for (; t - 1 >= 0; t -= 2) {
-      step(t, sa, sb);
-      step(t - 1, sb, sa);
+    if (VAR & 8) {   // diagnostic only: chain cycles per step, binned by the producer phase u = 15 - (t & 15)
+      uint64_t bins[FCH];
+#pragma unroll
+      for (int i = 0; i < FCH; ++i) bins[i] = 0;
+      const uint64_t c0 = __builtin_amdgcn_s_memtime();
+      for (; t >= 0; t -= 2) {
+        const uint64_t a0 = __builtin_amdgcn_s_memtime();
+        step(t, sa, sb);
+        const uint64_t a1 = __builtin_amdgcn_s_memtime();
+        if (t - 1 >= 0) step(t - 1, sb, sa);
+        const uint64_t a2 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+        for (int i = 0; i < FCH; ++i) {
+          if (i == FCH - 1 - (t & (FCH - 1))) bins[i] += a1 - a0;
+          if (t - 1 >= 0 && i == FCH - 1 - ((t - 1) & (FCH - 1))) bins[i] += a2 - a1;
+        }
+      }
+      if (tid == 0) {
+        uint64_t* st = (uint64_t*)w.slab_mix + 32 * blockIdx.x;
+#pragma unroll
+        for (int i = 0; i < FCH; ++i) st[i] = bins[i];
+        st[16] = __builtin_amdgcn_s_memtime() - c0;
+      }
+    } else {
+      for (; t - 1 >= 0; t -= 2) {
+        step(t, sa, sb);
+        step(t - 1, sb, sa);
+      }
+      if (t >= 0) step(t, sa, sb);
     }
-    if (t >= 0) step(t, sa, sb);
     lds_barrier();   // producer tail: chunk 0 (2 barriers)
     lds_barrier();
     if (q < 3) { slab[o_bi + q * H + k] = db_i; slab[o_bh + q * H + k] = db_h; }

@@ -104,14 +104,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   if (rec) {
     // ================================================================ recurrence waves
     const int j = tid >> 2, q = tid & 3;
-    float wr[16], wz[16], wn[16];
+    f32x2 wr[8], wz[8], wn[8];   // W_hh[gate * 64 + j][16 q .. 16 q + 15] as pairs for v_pk_fma_f32
     {
       const float* Whh = P + L.o[MQ_P_RNN_W_HH];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        wr[k] = Whh[(0 * H + j) * H + 16 * q + k];
-        wz[k] = Whh[(1 * H + j) * H + 16 * q + k];
-        wn[k] = Whh[(2 * H + j) * H + 16 * q + k];
+      for (int k = 0; k < 8; ++k) {
+        wr[k] = f32x2{Whh[(0 * H + j) * H + 16 * q + 2 * k], Whh[(0 * H + j) * H + 16 * q + 2 * k + 1]};
+        wz[k] = f32x2{Whh[(1 * H + j) * H + 16 * q + 2 * k], Whh[(1 * H + j) * H + 16 * q + 2 * k + 1]};
+        wn[k] = f32x2{Whh[(2 * H + j) * H + 16 * q + 2 * k], Whh[(2 * H + j) * H + 16 * q + 2 * k + 1]};
       }
     }
     const float bhr = P[L.o[MQ_P_RNN_B_HH] + j], bhz = P[L.o[MQ_P_RNN_B_HH] + H + j],
@@ -127,21 +127,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       float sr, sz, sn;
       {
         const f32x4* hv4 = (const f32x4*)(&hb[16 * q]);
-        float ar = 0.0f, az = 0.0f, an = 0.0f, ar2 = 0.0f, az2 = 0.0f, an2 = 0.0f;
+        f32x2 ar = {0.0f, 0.0f}, az = {0.0f, 0.0f}, an = {0.0f, 0.0f};
 #pragma unroll
         for (int k4 = 0; k4 < 4; ++k4) {
           const f32x4 hv = hv4[k4];
-#pragma unroll
-          for (int e = 0; e < 4; e += 2) {
-            const int k = 4 * k4 + e;
-            ar = fmaf(wr[k], hv[e], ar); ar2 = fmaf(wr[k + 1], hv[e + 1], ar2);
-            az = fmaf(wz[k], hv[e], az); az2 = fmaf(wz[k + 1], hv[e + 1], az2);
-            an = fmaf(wn[k], hv[e], an); an2 = fmaf(wn[k + 1], hv[e + 1], an2);
-          }
+          const f32x2 h01 = {hv[0], hv[1]}, h23 = {hv[2], hv[3]};
+          ar = pk_fma(wr[2 * k4], h01, ar); ar = pk_fma(wr[2 * k4 + 1], h23, ar);
+          az = pk_fma(wz[2 * k4], h01, az); az = pk_fma(wz[2 * k4 + 1], h23, az);
+          an = pk_fma(wn[2 * k4], h01, an); an = pk_fma(wn[2 * k4 + 1], h23, an);
         }
-        sr = quad_sum(ar + ar2);
-        sz = quad_sum(az + az2);
-        sn = quad_sum(an + an2);
+        sr = quad_sum(ar.x + ar.y);
+        sz = quad_sum(az.x + az.y);
+        sn = quad_sum(an.x + an.y);
       }
       // lane-split gate math (as gru_fwd_body<1>): lane 0 r, lane 1 z, lane 2 n; lane q stores component q
       const float gh = q == 0 ? sr + bhr : (q == 1 ? sz + bhz : 0.0f);

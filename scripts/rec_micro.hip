@@ -4,7 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
-#include "../pymarl_amd/csrc/gru_fwd_fused.hpp"
+#include "../pymarl_amd/csrc/gru_bwd_fused.hpp"
 using namespace mq;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
@@ -133,6 +133,34 @@ int main(int argc, char** argv) {
         double c = 0; for (int i = 0; i < 2 * d.R; ++i) c += sb[16 * i + p];
         const int cnt = nch - (p >= d.Tp - 16 * (nch - 1) ? 1 : 0);
         printf(" %.0f", c / (2 * d.R) / cnt);
+      }
+      printf("\n");
+    }
+  }
+  {  // fused BPTT
+    int64_t len1 = 64 * d.I + 64;
+    CK(hipMalloc(&w.slab_fc1, (int64_t)d.R * len1 * 4));
+    float* obs = dev_rand((int64_t)B * (T + 1) * n * O, 1.0f);
+    Rep rf = rp; rf.obs = obs;
+    if (!w.XIN) CK(hipMalloc(&w.XIN, RT * d.I * 4));
+    CK(hipMemset(w.XIN, 0, RT * d.I * 4));
+    auto runbf = [&](auto kern) {
+      size_t dyn = (2 * A * 64 + A) * 4;
+      return time_it([&] { hipLaunchKernelGGL(kern, dim3(d.R), dim3(512), dyn, 0, d, rf, (const float*)P0, L, w, len_rnn, len1); });
+    };
+    printf("fused bwd %.1f us\n", runbf(gru_bwd_fused_kernel<0>));
+    printf("fused bwd V4(no producer MFMA) %.1f us\n", runbf(gru_bwd_fused_kernel<4>));
+    CK(hipFree(w.slab_mix)); CK(hipMalloc(&w.slab_mix, 32 * 8 * d.R));
+    for (int var : {8, 12}) {
+      if (var == 8) runbf(gru_bwd_fused_kernel<8>); else runbf(gru_bwd_fused_kernel<12>);
+      std::vector<uint64_t> sb(32 * d.R);
+      CK(hipMemcpy(sb.data(), w.slab_mix, sb.size() * 8, hipMemcpyDeviceToHost));
+      double tot = 0; for (int i = 0; i < d.R; ++i) tot += sb[32 * i + 16];
+      printf("fused bwd V%d loop %.0f cycles/step; by phase u:", var, tot / d.R / d.Tp);
+      const int nch = (d.Tp + 15) / 16;
+      for (int u = 0; u < 16; ++u) {
+        double c = 0; for (int i = 0; i < d.R; ++i) c += sb[32 * i + u];
+        printf(" %.0f", c / d.R / nch);
       }
       printf("\n");
     }
