@@ -11,10 +11,11 @@ full train(): id sampling on the host, fused gather, both unrolls, double-Q, mix
 the episode-counted target update — nothing skipped.
 
 The JSON line also carries:
-* roofline: the dominant kernel (longest mean duration over the timed steps, HIP events on the learner's stream)
-  priced by its ALGORITHMIC fp32 flops per launch (DESIGN.md "Roofline") against the gfx950 fp32 peak;
-  `traffic` = PMC-measured HBM bytes per launch of that kernel, read from profiles/ if a pmc summary for this
-  config is committed there (null otherwise).
+* roofline: the dominant kernel (longest mean duration in an untimed 4-step phase survey) priced by its
+  ALGORITHMIC fp32 flops per launch (DESIGN.md "Roofline") against the gfx950 fp32 peak; its average launch
+  duration comes from HIP events on the learner's stream over a second timed region of the same K steps (the
+  first timed region, which gives `value`, carries no events); `traffic` = PMC-measured HBM bytes per launch of
+  that kernel, read from profiles/ if a pmc summary for this config is committed there (null otherwise).
 * cpu_baseline: the numpy oracle's train() (oracle/qlearner_np.py, a restatement of the reference's QLearner.train
   pinned to golden vectors of the reference itself) timed on this host, rank 0 at N=1 only, on a bounded sample.
 """
@@ -45,8 +46,12 @@ CONFIGS = {
 }
 
 
-def algorithmic_flops(phase, n, A, O, S, T, B, E=32, H=64, mixer="qmix"):
-    """fp32 flops one launch of `phase` must do (matmul terms, 2 flop per MAC; elementwise ignored)."""
+def algorithmic_flops(phase, n, A, O, S, T, B, E=32, H=64, mixer="qmix", fused_fwd=False, fused_bwd=False):
+    """fp32 flops one launch of `phase` must do (matmul terms, 2 flop per MAC; elementwise ignored).
+
+    fused_fwd / fused_bwd: the one-row-per-workgroup kernels also carry fc1 / W_ih / fc2 (forward) and
+    dW_hh / dW_ih / dX1 / dW1 (backward) — DESIGN.md "Roofline".
+    """
     Tp = T + 1
     R = B * n
     RT = Tp * R
@@ -64,6 +69,10 @@ def algorithmic_flops(phase, n, A, O, S, T, B, E=32, H=64, mixer="qmix"):
         "dw1": 2 * RT * H * I,
         "dwh": 2 * M * NH * S if mixer == "qmix" else 0,
     }
+    if fused_fwd:
+        f["gru_fwd"] = f["fc1"] + f["gi"] + f["gru_fwd"] + f["fc2"]
+    if fused_bwd:
+        f["gru_bwd"] = f["gru_bwd"] + f["dx1"] + f["dw1"]
     return f.get(phase)
 
 
@@ -212,16 +221,25 @@ def main():
     th.cuda.synchronize()
     survey = learner.phase_times()
     dominant = max(survey, key=survey.get)
-    # timed region: events around the dominant kernel only
+    fused_fwd = survey.get("fc1", 0.0) == 0.0     # the fused agent forward carries fc1 / W_ih / fc2
+    fused_bwd = survey.get("dx1", 0.0) == 0.0     # the fused BPTT carries dX1 / dW1
+
+    def timed():
+        barrier()
+        th.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(a.steps):
+            step(k)
+        th.cuda.synchronize()
+        barrier()
+        return time.perf_counter() - t0
+
+    # timed region 1 -> value: no events in the stream
+    learner.set_timing(slots=0)
+    dt = timed()
+    # timed region 2 -> roofline: the same K steps with HIP events (learner stream) around the dominant kernel
     learner.set_timing(slots=min(a.steps, 4096), phases=[dominant])
-    barrier()
-    th.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(a.steps):
-        step(k)
-    th.cuda.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
+    timed()
     dom_ms = learner.phase_times()[dominant]
     learner.set_timing(slots=0)
     if world > 1:
@@ -234,12 +252,13 @@ def main():
     if rank == 0:
         if a.phases:
             print(json.dumps({"phase_ms": survey}), file=sys.stderr)
-        fl = algorithmic_flops(dominant, n, A, O, S, T, B, mixer=mixer)
+        fl = algorithmic_flops(dominant, n, A, O, S, T, B, mixer=mixer, fused_fwd=fused_fwd, fused_bwd=fused_bwd)
         achieved = (fl / (dom_ms * 1e-3) / 1e12) if (fl and dom_ms > 0) else None
         traffic = pmc_traffic(a.config, dominant)
         roof = {"bound": "mfma", "kernel": dominant, "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": (achieved / FP32_PEAK_TFLOPS) if achieved else None,
-                "traffic": traffic, "launch_ms": dom_ms, "flops_per_launch": fl}
+                "traffic": traffic, "launch_ms": dom_ms, "flops_per_launch": fl,
+                "fused": {"fwd": fused_fwd, "bwd": fused_bwd}}
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(a.config, data)
