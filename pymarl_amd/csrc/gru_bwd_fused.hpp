@@ -56,7 +56,15 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
   float* dw2_s = dyn + A * H;
   float* db2_s = dyn + 2 * A * H;
 
-  for (int i = tid; i < A * H; i += 512) { w2_s[i] = P[L.o[MQ_P_FC2_W] + i]; dw2_s[i] = 0.0f; }
+  {
+    constexpr int NW2 = 16 * H / 512;   // A <= 16: all W2 loads in flight before the stores
+    float v[NW2];
+#pragma unroll
+    for (int u = 0; u < NW2; ++u) v[u] = tid + 512 * u < A * H ? P[L.o[MQ_P_FC2_W] + tid + 512 * u] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < NW2; ++u)
+      if (tid + 512 * u < A * H) { w2_s[tid + 512 * u] = v[u]; dw2_s[tid + 512 * u] = 0.0f; }
+  }
   for (int i = tid; i < A; i += 512) db2_s[i] = 0.0f;
   // zero the history rows past Tp of the top (partial) chunk and the XIN padding
   for (int e = tid; e < 2 * FCH * BRP; e += 512) { (&S.gh[0][0][0])[e] = 0.0f; (&S.gi[0][0][0])[e] = 0.0f; }
@@ -88,26 +96,33 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
 #pragma unroll
       for (int c = 0; c < 24; ++c) wT[c] = f32x2{Whh[(48 * q + 2 * c) * H + k], Whh[(48 * q + 2 * c + 1) * H + k]};
     }
-    // lane-split inputs of a step: lane q loads gate component q and one of (h_{t-1}, -, dch, action)
+    // lane-split inputs of a step: lane q loads gate component q and one of (h_{t-1}, dch, dch, action). Each
+    // lane's second address is base + idx(t) * stride with per-lane constants, so no lane-dependent branch
+    // enters the chain (the action is read as the low word of the int64, little-endian, 0 <= a < A).
     struct In { float g, aux; };
+    const float* aux_base;
+    int64_t aux_stride;
+    if (q == 0) { aux_base = w.Hs + (int64_t)r * H + k - (int64_t)R * H; aux_stride = (int64_t)R * H; }
+    else if (q == 3) { aux_base = (const float*)arow; aux_stride = 2 * (int64_t)d.n; }
+    else { aux_base = w.dch + r; aux_stride = R; }
+    const float* g_base = w.Gates + (int64_t)r * (4 * H) + q * H + k;
     auto load = [&](int t, In& s) {
-      const int tc = max(t, 0), td = min(tc, T - 1);
-      const int64_t tr = (int64_t)tc * R + r;
-      const float* src = q == 0   ? w.Hs + (tc > 0 ? tr - R : tr) * H + k
-                         : q == 3 ? (const float*)(arow + (int64_t)tc * d.n)
-                                  : w.dch + (int64_t)td * R + r;
-      s.g = w.Gates[tr * (4 * H) + q * H + k];
-      s.aux = *src;
+      const int tc = max(t, 0);
+      const int idx = q == 0 ? max(tc, 1) : (q == 3 ? tc : min(tc, T - 1));   // h_{t-1} (row 0 stands in at t = 0)
+      s.g = g_base[(int64_t)tc * R * (4 * H)];
+      s.aux = aux_base[idx * aux_stride];
     };
+    // lane-split selectors as 0/1 factors (multiply-add selects, no branches)
+    const float m0 = q == 0 ? 1.0f : 0.0f, m1 = q == 1 ? 1.0f : 0.0f, m2 = q == 2 ? 1.0f : 0.0f;
+    const float m3 = q == 3 ? 1.0f : 0.0f;
     float carry = 0.0f, db_i = 0.0f, db_h = 0.0f;   // bias grads: this lane's component q of b_ih / b_hh
     auto step = [&](int t, const In& cur, In& nxt) {
       load(t - 1, nxt);   // previous (earlier) step's inputs, in flight under this step
       const int p = t & (FCH - 1), cb = (t / FCH) & 1, pb = t & 1;
-      const bool live = t < Tp;
       const float gr = quad_bcast<0>(cur.g), gz = quad_bcast<1>(cur.g), gn = quad_bcast<2>(cur.g),
                   ghn = quad_bcast<3>(cur.g);
       const float hp = t > 0 ? quad_bcast<0>(cur.aux) : 0.0f;
-      const float dchv = (live && t < T) ? quad_bcast<2>(cur.aux) : 0.0f;
+      const float dchv = t < T ? quad_bcast<2>(cur.aux) : 0.0f;
       const int a = __builtin_bit_cast(int, quad_bcast<3>(cur.aux));
       const float dh = carry + dchv * w2_s[a * H + k];
       if (k == 0 && q == 0) { S.dch[pb] = dchv; S.act[pb] = a; }
@@ -116,12 +131,13 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       const float dan = dn * (1.0f - gn * gn);
       const float dar = (dan * ghn) * (gr * (1.0f - gr));
       const float daz = dz * (gz * (1.0f - gz));
-      const float mine_i = q == 0 ? dar : (q == 1 ? daz : dan);   // dgi component q
-      const float mine_h = q == 2 ? dan * gr : mine_i;             // dgh component q
-      S.gh[cb][p][q * H + k] = q < 3 ? mine_h : hp;
+      const float rz = fmaf(m0, dar, m1 * daz);
+      const float mine_i = fmaf(m2 + m3, dan, rz);                   // dgi component q (q = 3: unused slot)
+      const float mine_h = fmaf(m2, dan * gr, fmaf(m3, hp, rz));     // dgh component q, or h_{t-1} at q = 3
+      S.gh[cb][p][q * H + k] = mine_h;
       S.gi[cb][p][q * H + k] = mine_i;
-      db_i += q < 3 ? mine_i : 0.0f;
-      db_h += q < 3 ? mine_h : 0.0f;
+      db_i = fmaf(1.0f - m3, mine_i, db_i);
+      db_h = fmaf(1.0f - m3, mine_h, db_h);
       const float cz = dh * gz;
       lds_barrier();
       // dh_{t-1} = dh * z + W_hh^T dgh

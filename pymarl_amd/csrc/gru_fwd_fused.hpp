@@ -120,10 +120,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     for (int i = 0; i < 5; ++i) lds_barrier();   // the producers' chunk-0 prologue (5 barriers)
     float* Hz = w.Hs;   // online only: the backward pass reads h_{t-1}
     const int gcol = min(q, 2) * H + j;
-    float own = S.gi[0][0][gcol];   // this step's input gate, read right after the previous step's barrier
+    // lane-split selectors as 0/1 factors: select by multiply-add, so no lane-dependent branch enters the chain
+    const float m0 = q == 0 ? 1.0f : 0.0f, m1 = q == 1 ? 1.0f : 0.0f, m2 = q == 2 ? 1.0f : 0.0f;
+    const float m3 = q == 3 ? 1.0f : 0.0f;
+    const float bsel = m0 * bhr + m1 * bhz;
+    float hprev = 0.0f;   // h_{t-1}[j]: every lane of the quad computes unit j's h, so it never re-reads LDS
     auto step = [&](int t) {
       const int p = t & (FCH - 1), c = t / FCH;
       const float* hb = t == 0 ? S.h0 : S.hs[((t - 1) / FCH) & 1][(t - 1) & (FCH - 1)];
+      const float own = S.gi[c & 1][p][gcol];   // issued with the h reads below (same LDS latency window)
       float sr, sz, sn;
       {
         const f32x4* hv4 = (const f32x4*)(&hb[16 * q]);
@@ -141,22 +146,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         sn = quad_sum(an.x + an.y);
       }
       // lane-split gate math (as gru_fwd_body<1>): lane 0 r, lane 1 z, lane 2 n; lane q stores component q
-      const float gh = q == 0 ? sr + bhr : (q == 1 ? sz + bhz : 0.0f);
+      const float gh = fmaf(m0, sr, fmaf(m1, sz, bsel));
       const float sg = sigm_fast(gh + own);
       const float rg = quad_bcast<0>(sg), zg = quad_bcast<1>(sg);
       const float ghn = sn + bhn;
       const float ng = quad_bcast<2>(tanh_fast(own + ghn * rg));
-      const float hp = hb[j];
-      const float h1 = (hp - ng) * zg + ng;   // ATen gru_cell: (hx - n) * z + n
+      const float h1 = (hprev - ng) * zg + ng;   // ATen gru_cell: (hx - n) * z + n
+      hprev = h1;
       if (q == 0) S.hs[c & 1][p][j] = h1;
       if (online && !(VAR & 1)) {
         const int64_t tr = (int64_t)t * R + r;
         if (q == 0) Hz[tr * H + j] = h1;
-        w.Gates[tr * (4 * H) + q * H + j] = q == 0 ? rg : (q == 1 ? zg : (q == 2 ? ng : ghn));
+        w.Gates[tr * (4 * H) + q * H + j] = fmaf(m0, rg, fmaf(m1, zg, fmaf(m2, ng, m3 * ghn)));
       }
       lds_barrier();
-      const int t1 = t + 1;
-      own = S.gi[(t1 / FCH) & 1][t1 & (FCH - 1)][gcol];
     };
     uint64_t c0 = 0, r0t = 0;
     if (VAR & 2) { c0 = __builtin_amdgcn_s_memtime(); r0t = __builtin_amdgcn_s_memrealtime(); }

@@ -112,13 +112,17 @@ int main(int argc, char** argv) {
       CK(hipMemcpy(sb.data(), w.slab_mix, sb.size() * 8, hipMemcpyDeviceToHost));
       uint64_t t0 = ~0ull;
       for (int i = 0; i < 2 * d.R; ++i) t0 = std::min(t0, sb[16 * i]);
-      printf("fused prologue milestones (us after the earliest WG start, mean / max over WGs):");
-      for (int k = 0; k <= 8; ++k) {
-        double m = 0, mx = 0;
-        for (int i = 0; i < 2 * d.R; ++i) { double v = (sb[16 * i + k] - t0) / 100.0; m += v; mx = std::max(mx, v); }
-        printf(" [%d] %.2f/%.2f", k, m / (2 * d.R), mx);
+      for (int net = 0; net < 2; ++net) {
+        printf("fused prologue milestones net %d (us after the earliest WG start, mean / max over WGs):", net);
+        for (int k = 0; k <= 8; ++k) {
+          double m = 0, mx = 0;
+          for (int i = net * d.R; i < (net + 1) * d.R; ++i) {
+            double v = (sb[16 * i + k] - t0) / 100.0; m += v; mx = std::max(mx, v);
+          }
+          printf(" [%d] %.2f/%.2f", k, m / d.R, mx);
+        }
+        printf("\n");
       }
-      printf("\n");
     }
     for (int var : {8, 12}) {
       CK(hipFree(w.slab_mix)); CK(hipMalloc(&w.slab_mix, 16 * 8 * 2 * d.R));
