@@ -215,7 +215,8 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       }
 #pragma unroll
       for (int s = 0; s < NXI; ++s) {
-        const int e = opaque(ptid + 256 * s), i = e / I, col = e - i * I, t = min(t0 + i, Tp - 1);
+        const int e = opaque(ptid + 256 * s), i = (int)fdiv((uint32_t)e, d.dI), col = e - i * I;
+        const int t = min(t0 + i, Tp - 1);
         rxi[s] = e < FCH * I ? w.XIN[((int64_t)t * R + r) * I + col] : 0.0f;
       }
     };
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       }
 #pragma unroll
       for (int s = 0; s < NXI; ++s) {
-        const int e = opaque(ptid + 256 * s), i = e / I, col = e - i * I;
+        const int e = opaque(ptid + 256 * s), i = (int)fdiv((uint32_t)e, d.dI), col = e - i * I;
         if (e < FCH * I) S.xin[i][col] = t0 + i < Tp ? rxi[s] : 0.0f;
       }
     };

@@ -219,7 +219,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   int gsl[FGATHER];
 #pragma unroll
   for (int s = 0; s < FGATHER; ++s) {
-    const int e = ptid + 256 * s, i = e / O;
+    const int e = ptid + 256 * s, i = (int)fdiv((uint32_t)e, d.dO);
     gsl[s] = e < FCH * O ? (i << 16) | (i * n * O + e - i * O) : -1;
   }
   const int nO = n * O;

@@ -129,6 +129,8 @@ Dims make_dims(const mq_handle* h, const mq_replay* b) {
   d.dR = make_fastdiv((uint32_t)d.R);
   d.dN = make_fastdiv((uint32_t)d.n);
   d.dB = make_fastdiv((uint32_t)d.B);
+  d.dO = make_fastdiv((uint32_t)d.O);
+  d.dI = make_fastdiv((uint32_t)d.I);
   return d;
 }
 

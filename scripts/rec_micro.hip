@@ -34,6 +34,7 @@ int main(int argc, char** argv) {
   d.B = B; d.Tp = T + 1; d.T = T; d.R = B * n; d.M = T * B; d.t_stride = T + 1;
   d.last_action = 1; d.agent_id = 1; d.mixer = 2; d.double_q = 1; d.gamma = 0.99f;
   d.dR = make_fastdiv(d.R); d.dN = make_fastdiv(n); d.dB = make_fastdiv(B);
+  d.dO = make_fastdiv(O); d.dI = make_fastdiv(d.I);
   const int64_t RT = (int64_t)d.Tp * d.R;
   Lay L{};
   int64_t o = 0, sz[MQ_P_COUNT] = {};
