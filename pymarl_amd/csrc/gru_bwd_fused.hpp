@@ -33,8 +33,6 @@ struct BwdFusedLds {
   float dx1[FCH][H + 4];     // dX1 of the chunk being reduced
   float db1[4][H];           // fc1 bias-grad partials of the four lane groups
   float wih[G3][H + 1];      // W_ih (dX1's B operand); odd pitch: the four lane groups read rows 48 apart
-  float dch[2];              // this step's dLoss/dchosen (0 at t = T) and action, for the fc2 grads
-  int act[2];
 };
 
 inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_fwd_ok(I, O, A, n, RT); }
@@ -96,36 +94,39 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
 #pragma unroll
       for (int c = 0; c < 24; ++c) wT[c] = f32x2{Whh[(48 * q + 2 * c) * H + k], Whh[(48 * q + 2 * c + 1) * H + k]};
     }
-    // lane-split inputs of a step: lane q loads gate component q and one of (h_{t-1}, dch, dch, action). Each
-    // lane's second address is base + idx(t) * stride with per-lane constants, so no lane-dependent branch
-    // enters the chain (the action is read as the low word of the int64, little-endian, 0 <= a < A).
-    struct In { float g, aux; };
+    // lane-split inputs of a step: lane q loads gate component q and one of (h_{t-1}, dch, dch, action) at
+    // base + idx * stride with per-lane constants, so no lane-dependent branch enters the chain. idx = t except
+    // at the edges, clamped with per-lane 0/1 flags: h row 0 stands in for row -1 at t = 0 (hp is zeroed there),
+    // dch row T-1 for row T at t = T (dchv is zeroed there). The action is read as the low word of the int64
+    // (little-endian, 0 <= a < A). w2 = W2[a_t][k] is looked up one step ahead (end of the previous step), off
+    // the dh chain.
+    struct In { float g, aux, w2; };
     const float* aux_base;
     int64_t aux_stride;
     if (q == 0) { aux_base = w.Hs + (int64_t)r * H + k - (int64_t)R * H; aux_stride = (int64_t)R * H; }
     else if (q == 3) { aux_base = (const float*)arow; aux_stride = 2 * (int64_t)d.n; }
     else { aux_base = w.dch + r; aux_stride = R; }
     const float* g_base = w.Gates + (int64_t)r * (4 * H) + q * H + k;
+    const int e0 = q == 0 ? 1 : 0, e12 = (q == 1 || q == 2) ? 1 : 0;
     auto load = [&](int t, In& s) {
       const int tc = max(t, 0);
-      const int idx = q == 0 ? max(tc, 1) : (q == 3 ? tc : min(tc, T - 1));   // h_{t-1} (row 0 stands in at t = 0)
+      const int idx = tc + (e0 & (tc == 0 ? 1 : 0)) - (e12 & (tc >= T ? 1 : 0));
       s.g = g_base[(int64_t)tc * R * (4 * H)];
       s.aux = aux_base[idx * aux_stride];
     };
+    auto lookup_w2 = [&](In& s) { s.w2 = w2_s[__builtin_bit_cast(int, quad_bcast<3>(s.aux)) * H + k]; };
     // lane-split selectors as 0/1 factors (multiply-add selects, no branches)
     const float m0 = q == 0 ? 1.0f : 0.0f, m1 = q == 1 ? 1.0f : 0.0f, m2 = q == 2 ? 1.0f : 0.0f;
     const float m3 = q == 3 ? 1.0f : 0.0f;
     float carry = 0.0f, db_i = 0.0f, db_h = 0.0f;   // bias grads: this lane's component q of b_ih / b_hh
     auto step = [&](int t, const In& cur, In& nxt) {
       load(t - 1, nxt);   // previous (earlier) step's inputs, in flight under this step
-      const int p = t & (FCH - 1), cb = (t / FCH) & 1, pb = t & 1;
+      const int p = t & (FCH - 1), cb = (t / FCH) & 1;
       const float gr = quad_bcast<0>(cur.g), gz = quad_bcast<1>(cur.g), gn = quad_bcast<2>(cur.g),
                   ghn = quad_bcast<3>(cur.g);
       const float hp = t > 0 ? quad_bcast<0>(cur.aux) : 0.0f;
       const float dchv = t < T ? quad_bcast<2>(cur.aux) : 0.0f;
-      const int a = __builtin_bit_cast(int, quad_bcast<3>(cur.aux));
-      const float dh = carry + dchv * w2_s[a * H + k];
-      if (k == 0 && q == 0) { S.dch[pb] = dchv; S.act[pb] = a; }
+      const float dh = carry + dchv * cur.w2;
       const float dn = dh * (1.0f - gz);
       const float dz = dh * (hp - gn);
       const float dan = dn * (1.0f - gn * gn);
@@ -150,11 +151,13 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
         a23 = pk_fma(wT[2 * c4 + 1], f32x2{dg[2], dg[3]}, a23);
       }
       carry = cz + quad_sum((a01.x + a01.y) + (a23.x + a23.y));
+      lookup_w2(nxt);
     };
     In sa, sb;
     load(Tp - 1, sa);
     drain_vmem();
     lds_barrier();
+    lookup_w2(sa);
     int t = Tp - 1;
     if (VAR & 8) {   // diagnostic only: chain cycles per step, binned by the producer phase u = 15 - (t & 15)
       uint64_t bins[FCH];
@@ -292,19 +295,27 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     };
     // fc2 grads of step t: dW2[a][k] += dchosen * h_t[k]; (a, k) owned by lane (k, q = a % 4); h_t was the
     // h_{t-1} record of step t+1
-    float h_next = 0.0f;
+    // fc2 grads of step t: dW2[a][k] += dchosen * h_t[k]; (a, k) owned by lane (k, q = a % 4); h_t was the
+    // h_{t-1} record of step t+1. dchosen_t and a_t are wave-uniform loads issued one step ahead.
+    float h_next = 0.0f, dch_n = 0.0f;
+    int act_n = 0;
+    auto fc2_fetch = [&](int t) {
+      const int tc = max(t, 0);
+      dch_n = w.dch[(int64_t)min(tc, T - 1) * R + r];
+      act_n = *(const int*)(arow + (int64_t)tc * d.n);
+    };
     auto fc2_grads = [&](int t) {
-      const int pb = t & 1, p = t & (FCH - 1), cb = (t / FCH) & 1;
-      if (t < T) {
-        const int a = S.act[pb];
-        if ((a & 3) == q) {
-          const float dchv = S.dch[pb];
-          dw2_s[a * H + k] += dchv * h_next;
-          if (k == 0) db2_s[a] += dchv;
-        }
+      const int p = t & (FCH - 1), cb = (t / FCH) & 1;
+      const float dchv = t < T ? dch_n : 0.0f;
+      const int a = act_n;
+      fc2_fetch(t - 1);
+      if (t < T && (a & 3) == q) {
+        dw2_s[a * H + k] += dchv * h_next;
+        if (k == 0) db2_s[a] += dchv;
       }
       h_next = S.gh[cb][p][3 * H + k];
     };
+    fc2_fetch(Tp - 1);
 
     lds_barrier();
     for (int c = cl; c >= 0; --c) {
