@@ -14,7 +14,7 @@ struct Dims {
   int t_stride;              // storage max_seq_length
   int last_action, agent_id, mixer, double_q;
   float gamma;
-  FastDiv dR, dN, dB, dO, dI;   // fast division by R, n, B, obs width, agent input width
+  FastDiv dR, dN, dB, dO, dI, dS;   // fast division by R, n, B, obs / agent-input / state widths
   MQ_DEV int64_t RT() const { return (int64_t)Tp * R; }
 };
 

@@ -27,6 +27,7 @@
 #include "gru_fwd_fused.hpp"
 #include "gru_bwd_fused.hpp"
 #include "mix_kernels.hpp"
+#include "hyper_kernel.hpp"
 #include "optim_kernels.hpp"
 
 using namespace mq;
@@ -82,6 +83,7 @@ struct mq_handle {
   int nsplit_fc1 = 1, nsplit_mix = 1, nblk_bwd = 1, nblk_mix = 1, n_norm_part = 0;
   bool force_unfused = getenv("MQ_UNFUSED_FWD") != nullptr;       // A/B switch for the fused agent forward
   bool force_unfused_bwd = getenv("MQ_UNFUSED_BWD") != nullptr;   // A/B switch for the fused BPTT
+  bool force_unfused_mix = getenv("MQ_GEMM_HYPER") != nullptr;   // A/B switch: hypernet through gemm_f32
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
   int slots = 0;
@@ -131,6 +133,7 @@ Dims make_dims(const mq_handle* h, const mq_replay* b) {
   d.dB = make_fastdiv((uint32_t)d.B);
   d.dO = make_fastdiv((uint32_t)d.O);
   d.dI = make_fastdiv((uint32_t)d.I);
+  d.dS = make_fastdiv((uint32_t)std::max(d.S, 1));
   return d;
 }
 
@@ -381,8 +384,15 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   }
   if (c.mixer == MQ_MIXER_QMIX) {
     pt.begin(PH_HYP);
-    HypProb p{d, rp, L, h->on, h->tg, w.HYP, w.S0};
-    MQ_HIP(launch_gemm(p, d.M, d.NH, 2, s));
+    if (hyper_ok(d.S, d.NH) && !h->force_unfused_mix) {
+      const size_t dyn = HyperGeom(d.S, d.NH).lds_bytes();
+      hipLaunchKernelGGL(hyper_kernel<0>, dim3((d.M + HYR - 1) / HYR, 2), dim3(256), dyn, s, d, rp,
+                         (const float*)h->on, (const float*)h->tg, L, w.HYP, w.S0);
+      MQ_HIP(hipGetLastError());
+    } else {
+      HypProb p{d, rp, L, h->on, h->tg, w.HYP, w.S0};
+      MQ_HIP(launch_gemm(p, d.M, d.NH, 2, s));
+    }
   }
   pt.begin(PH_MIX);
   h->nblk_mix = (d.M + 3) / 4;

@@ -5,7 +5,7 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
-template <int MODE>   // 0: VALU waves alone, 1: + f32 MFMA waves, 2: + bf16 MFMA waves, 3: MFMA f32 alone
+template <int MODE>   // 0: VALU alone, 1: + f32 16x16x4 MFMA, 2: + bf16 MFMA, 3: f32 MFMA alone, 4: + f32 32x32x2
 __global__ __launch_bounds__(512) void k(float* out, int iters) {
   const int w = threadIdx.x >> 6;
   float a = threadIdx.x * 1e-3f, b = 1.0001f, c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0, c7 = 0;
@@ -26,7 +26,18 @@ __global__ __launch_bounds__(512) void k(float* out, int iters) {
     if (MODE == 0) return;
     f32x4 x0 = {0, 0, 0, 0}, x1 = x0, x2 = x0, x3 = x0;
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
-    if (MODE == 1 || MODE == 3) {
+    typedef float f32x16 __attribute__((ext_vector_type(16)));
+    if (MODE == 4) {
+      f32x16 y0 = {}, y1 = {};
+      for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, y0, 0, 0, 0);
+          y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, y1, 0, 0, 0);
+        }
+      }
+      x0[0] = y0[0] + y1[1];
+    } else if (MODE == 1 || MODE == 3) {
       for (int i = 0; i < iters; ++i) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -57,14 +68,15 @@ __global__ __launch_bounds__(512) void k(float* out, int iters) {
 int main() {
   float* out; hipMalloc(&out, 1 << 20);
   const int iters = 200;
-  const char* names[4] = {"VALU alone", "VALU + f32 MFMA", "VALU + bf16 MFMA", "f32 MFMA alone"};
-  for (int mode = 0; mode < 4; ++mode) {
+  const char* names[5] = {"VALU alone", "VALU + f32 MFMA", "VALU + bf16 MFMA", "f32 MFMA alone", "VALU + f32 32x32x2"};
+  for (int mode = 0; mode < 5; ++mode) {
     for (int rep = 0; rep < 2; ++rep) {
       hipMemset(out, 0, 1 << 20);
       if (mode == 0) hipLaunchKernelGGL(k<0>, dim3(256), dim3(512), 0, 0, out, iters);
       if (mode == 1) hipLaunchKernelGGL(k<1>, dim3(256), dim3(512), 0, 0, out, iters);
       if (mode == 2) hipLaunchKernelGGL(k<2>, dim3(256), dim3(512), 0, 0, out, iters);
       if (mode == 3) hipLaunchKernelGGL(k<3>, dim3(256), dim3(512), 0, 0, out, iters);
+      if (mode == 4) hipLaunchKernelGGL(k<4>, dim3(256), dim3(512), 0, 0, out, iters);
       hipDeviceSynchronize();
     }
     uint64_t st[256 * 8];

@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <vector>
 #include "../pymarl_amd/csrc/gru_bwd_fused.hpp"
+#include "../pymarl_amd/csrc/hyper_kernel.hpp"
 using namespace mq;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
@@ -40,6 +41,12 @@ int main(int argc, char** argv) {
   int64_t o = 0, sz[MQ_P_COUNT] = {};
   sz[MQ_P_FC1_W] = 64 * d.I; sz[MQ_P_FC1_B] = 64; sz[MQ_P_RNN_W_IH] = 192 * 64; sz[MQ_P_RNN_W_HH] = 192 * 64;
   sz[MQ_P_RNN_B_IH] = 192; sz[MQ_P_RNN_B_HH] = 192; sz[MQ_P_FC2_W] = A * 64; sz[MQ_P_FC2_B] = A;
+  {  // QMIX mixer params (for the hypernet kernel)
+    const int E = 32, S = d.S;
+    sz[MQ_P_HW1_W] = (int64_t)E * n * S; sz[MQ_P_HW1_B] = E * n; sz[MQ_P_HWF_W] = (int64_t)E * S; sz[MQ_P_HWF_B] = E;
+    sz[MQ_P_HB1_W] = (int64_t)E * S; sz[MQ_P_HB1_B] = E; sz[MQ_P_V0_W] = (int64_t)E * S; sz[MQ_P_V0_B] = E;
+    sz[MQ_P_V2_W] = E; sz[MQ_P_V2_B] = 1;
+  }
   for (int i = 0; i < MQ_P_COUNT; ++i) { L.o[i] = o; o += sz[i]; }
   L.o[MQ_P_COUNT] = o;
   float* P0 = dev_rand(o, 0.12f);
@@ -169,6 +176,25 @@ int main(int argc, char** argv) {
       }
       printf("\n");
     }
+  }
+  {  // hypernet
+    d.dS = make_fastdiv(d.S);
+    float* state = dev_rand((int64_t)B * (T + 1) * d.S, 1.0f);
+    Rep rh = rp; rh.state = state;
+    float *HYPb, *S0b;
+    CK(hipMalloc(&HYPb, (int64_t)2 * d.M * d.NH * 4)); CK(hipMalloc(&S0b, (int64_t)d.M * d.S * 4 + (1 << 20)));
+    const size_t dynh = HyperGeom(d.S, d.NH).lds_bytes();
+    dim3 gh((d.M + HYR - 1) / HYR, 2);
+    printf("hyper %.1f us\n", time_it([&] { hipLaunchKernelGGL(hyper_kernel<0>, gh, dim3(256), dynh, 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b); }));
+    hipLaunchKernelGGL(hyper_kernel<1>, gh, dim3(256), dynh, 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b);
+    CK(hipDeviceSynchronize());
+    const int nb = gh.x * gh.y;
+    std::vector<uint64_t> hs(8 * nb);
+    CK(hipMemcpy(hs.data(), S0b, hs.size() * 8, hipMemcpyDeviceToHost));
+    double a[7] = {0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < nb; ++i) for (int k = 0; k < 7; ++k) a[k] += hs[8 * i + k];
+    printf("hyper stamps (cycles, mean over %d WGs): first fetch %.0f, state gather %.0f, barriers %.0f, stores %.0f, fetch %.0f, mfma+epi %.0f, total %.0f\n",
+           nb, a[0] / nb, a[1] / nb, a[2] / nb, a[3] / nb, a[4] / nb, a[5] / nb, a[6] / nb);
   }
   printf("bwd RW1 %.1f us\n", runb(gru_bwd_kernel<1, 0>, 1));
   printf("bwd RW1 V4(cached inputs) %.1f us\n", runb(gru_bwd_kernel<1, 4>, 1));
