@@ -63,10 +63,15 @@ typedef struct mq_replay {
   const float* reward;         /* [N][t_stride][1] */
   const uint8_t* terminated;   /* [N][t_stride][1] */
   const int64_t* filled;       /* [N][t_stride][1] */
-  const int64_t* ep_ids;       /* [batch_size] episode ids; NULL = 0..batch_size-1 */
+  const int64_t* ep_ids;       /* [batch_size] episode ids (device); NULL = 0..batch_size-1 */
   int64_t n_episodes;
   int32_t batch_size, t_len, t_stride;
+  /* Optional HOST copy of the ids, read during the call: when set and batch_size <= MQ_INLINE_IDS the ids travel
+   * in the kernel arguments and ep_ids is not read (no host-to-device copy per step). */
+  const int64_t* ep_ids_host;
 } mq_replay;
+
+#define MQ_INLINE_IDS 256
 
 typedef struct mq_handle mq_handle;
 

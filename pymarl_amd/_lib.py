@@ -46,7 +46,11 @@ class MQReplay(ctypes.Structure):
         ("avail_actions", ctypes.c_void_p), ("reward", ctypes.c_void_p), ("terminated", ctypes.c_void_p),
         ("filled", ctypes.c_void_p), ("ep_ids", ctypes.c_void_p), ("n_episodes", ctypes.c_int64),
         ("batch_size", ctypes.c_int32), ("t_len", ctypes.c_int32), ("t_stride", ctypes.c_int32),
+        ("ep_ids_host", ctypes.c_void_p),
     ]
+
+
+INLINE_IDS = 256   # MQ_INLINE_IDS: batches up to this size pass their episode ids in the kernel arguments
 
 
 _LIB = None

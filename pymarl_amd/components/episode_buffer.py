@@ -189,12 +189,7 @@ class SampledBatch(EpisodeBatch):
     def __init__(self, source, ep_ids, t_len=None):
         self.source = source
         self.ep_ids_np = np.asarray(ep_ids, dtype=np.int64)
-        host = th.from_numpy(self.ep_ids_np)
-        if th.device(source.device).type == "cuda":
-            # pinned + async: the id upload is stream-ordered and never stalls the host on earlier kernels
-            self.ep_ids = host.pin_memory().to(source.device, non_blocking=True)
-        else:
-            self.ep_ids = host.to(source.device)
+        self._ep_ids_dev = None
         self.t_len = source.max_seq_length if t_len is None else int(t_len)
         super().__init__(source.scheme, source.groups, len(self.ep_ids_np), self.t_len,
                          data=SN(transition_data=_LazyGather(self, True), episode_data=_LazyGather(self, False)),
@@ -210,10 +205,23 @@ class SampledBatch(EpisodeBatch):
                 else self.data.transition_data[item]
         return self.materialize()[item]
 
+    @property
+    def ep_ids(self):
+        """Device copy of the ids, uploaded on first use (the learner passes small id sets in kernel arguments)."""
+        if self._ep_ids_dev is None:
+            host = th.from_numpy(self.ep_ids_np)
+            if th.device(self.source.device).type == "cuda":
+                # pinned + async: the id upload is stream-ordered and never stalls the host on earlier kernels
+                self._ep_ids_dev = host.pin_memory().to(self.source.device, non_blocking=True)
+            else:
+                self._ep_ids_dev = host.to(self.source.device)
+        return self._ep_ids_dev
+
     @classmethod
     def _view(cls, other, t_len):
         new = cls.__new__(cls)
-        new.source, new.ep_ids_np, new.ep_ids, new.t_len = other.source, other.ep_ids_np, other.ep_ids, int(t_len)
+        new.source, new.ep_ids_np, new.t_len = other.source, other.ep_ids_np, int(t_len)
+        new._ep_ids_dev = other._ep_ids_dev
         EpisodeBatch.__init__(new, other.source.scheme, other.source.groups, len(other.ep_ids_np), new.t_len,
                               data=SN(transition_data=_LazyGather(new, True), episode_data=_LazyGather(new, False)),
                               preprocess=None, device=other.source.device)

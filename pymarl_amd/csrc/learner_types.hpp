@@ -28,7 +28,9 @@ struct Rep {
   const uint8_t* term;
   const int64_t* filled;
   const int64_t* ep_ids;
-  MQ_DEV int64_t ep(int b) const { return ep_ids ? ep_ids[b] : (int64_t)b; }
+  int32_t nids;                    // > 0: the ids live in `ids` (kernel arguments), ep_ids unused
+  int32_t ids[MQ_INLINE_IDS];
+  MQ_DEV int64_t ep(int b) const { return nids ? (int64_t)ids[b] : (ep_ids ? ep_ids[b] : (int64_t)b); }
 };
 
 struct Lay {

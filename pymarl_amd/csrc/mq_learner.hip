@@ -141,6 +141,11 @@ Rep make_rep(const mq_replay* b) {
   Rep r;
   r.obs = b->obs; r.state = b->state; r.actions = b->actions; r.avail = b->avail_actions; r.reward = b->reward;
   r.term = b->terminated; r.filled = b->filled; r.ep_ids = b->ep_ids;
+  r.nids = 0;
+  if (b->ep_ids_host && b->batch_size <= MQ_INLINE_IDS) {   // ids in the kernel arguments (check_batch validated)
+    r.nids = b->batch_size;
+    for (int i = 0; i < b->batch_size; ++i) r.ids[i] = (int32_t)b->ep_ids_host[i];
+  }
   return r;
 }
 
@@ -162,6 +167,13 @@ int check_batch(const mq_handle* h, const mq_replay* b) {
     return set_err(MQ_ERR_ARG, "t_len " + std::to_string(b->t_len) + " must be in [2, min(max_seq, t_stride)]");
   if ((int64_t)b->t_len * b->batch_size * h->cfg.n_agents >= (1LL << 31))
     return set_err(MQ_ERR_ARG, "batch too large for 32-bit row indices");
+  if (b->ep_ids_host && b->batch_size <= MQ_INLINE_IDS) {
+    for (int i = 0; i < b->batch_size; ++i)
+      if (b->ep_ids_host[i] < 0 || b->ep_ids_host[i] >= b->n_episodes)
+        return set_err(MQ_ERR_ARG, "episode id " + std::to_string(b->ep_ids_host[i]) + " outside [0, n_episodes)");
+  } else if (!b->ep_ids && b->batch_size > b->n_episodes) {
+    return set_err(MQ_ERR_ARG, "batch_size exceeds n_episodes with no episode ids");
+  }
   return MQ_OK;
 }
 

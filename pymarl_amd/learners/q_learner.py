@@ -14,6 +14,8 @@ from __future__ import annotations
 
 import copy
 import ctypes
+
+import numpy as np
 import os
 
 import torch as th
@@ -78,9 +80,16 @@ def replay_view(batch):
     if isinstance(batch, SampledBatch):
         src = batch.source.data.transition_data
         tstride = batch.source.max_seq_length
-        ids = batch.ep_ids
-        keep.append(ids)
-        rep.ep_ids = ids.data_ptr()
+        if len(batch.ep_ids_np) <= _lib.INLINE_IDS:
+            # ids travel in the kernel arguments: no host-to-device copy on the step's stream
+            host = np.ascontiguousarray(batch.ep_ids_np, dtype=np.int64)
+            keep.append(host)
+            rep.ep_ids_host = host.ctypes.data
+            rep.ep_ids = None
+        else:
+            ids = batch.ep_ids
+            keep.append(ids)
+            rep.ep_ids = ids.data_ptr()
         rep.n_episodes = batch.source.batch_size
         rep.t_len = batch.t_len
         tensors = {}
