@@ -1,0 +1,98 @@
+// dW_hyper: the QMIX hypernet weight and bias gradients, summed over the M = T*B mixer rows
+//   dW[j][s] = sum_m dHYP[m][j] S0[m][s],   db[j] = sum_m dHYP[m][j]
+// (the backward of qmix.py:30-44's four state-fed Linear layers, in their concatenated order [hyper_w_1 |
+// hyper_w_final | hyper_b_1 | V.0], see hyp_seg).
+//
+// Both operands are stored m-major (one contiguous row of NH / S floats per mixer row), so the MFMA operands come
+// straight from global memory in v_mfma_f32_32x32x2_f32 layout with no LDS staging: lane l of a wave reads
+// S0[m + (l >> 5)][s0 + (l & 31)] (A, rows = s) and dHYP[m + (l >> 5)][j0 + (l & 31)] (B, columns = j) — two
+// 128-byte segments per operand per MFMA. The bias is a ones column appended to S0 (s == S), so db falls out of
+// the same accumulator. A workgroup owns a 32 (s) x 32 (j) output tile and one of `nsplit` slices of m; its four
+// waves take interleaved quarters of that slice and are summed through LDS, so each workgroup writes one partial
+// tile (coalesced along s) into slab[z] in the parameter layout relative to hyper_w_1.weight. red_pass1 sums the
+// nsplit partials. The m loop is branch-free: rows past the slice read a clamped row with a zero factor.
+#pragma once
+#include "learner_gemms.hpp"
+
+namespace mq {
+
+constexpr int DWH_T = 32;   // output tile edge
+constexpr int DWH_U = 8;    // MFMAs (2 m-rows each) per pipelined block
+
+// grid = ceil(NH / 32) * ceil((S + 1) / 32) * nsplit (tiles_j = ceil(NH / 32)), 256 threads.
+// VAR (scripts/rec_micro.hip only): 1 no MFMA, 2 no operand loads.
+template <int VAR = 0>
+__global__ __launch_bounds__(256) void dwh_kernel(Dims d, Lay L, const float* __restrict__ dHYP,
+                                                  const float* __restrict__ S0, float* __restrict__ slab,
+                                                  int64_t len, int nsplit, int tiles_j) {
+  __shared__ float red[4][DWH_T * (DWH_T + 1)];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int NH = d.NH, S = d.S, M = d.M;
+  // 1-D grid, slice-minor: consecutive workgroups go to consecutive XCDs, so with nsplit a multiple of 8 every
+  // workgroup of m-slice z runs on XCD z % 8 and the slice's dHYP / S0 rows are fetched into one L2 only
+  const int lin = blockIdx.x, z = lin % nsplit, tile = lin / nsplit;
+  const int j0 = (tile % tiles_j) * DWH_T, s0 = (tile / tiles_j) * DWH_T;
+  // m slice of this workgroup, in 2-row MFMA steps; wave wv takes steps wv, wv + 4, ..
+  const int steps = (M + 1) >> 1;
+  const int sb = (int)((int64_t)steps * z / nsplit), se = (int)((int64_t)steps * (z + 1) / nsplit);
+  const int half = lane >> 5, c = lane & 31;
+  const int jl = min(j0 + c, NH - 1);
+  const int s = s0 + c, sl = min(s, S - 1);
+  const float amul = s < S ? 1.0f : 0.0f, aadd = s == S ? 1.0f : 0.0f;
+
+  f32x16 acc = {};
+  float a0[DWH_U], b0[DWH_U], a1[DWH_U], b1[DWH_U];   // two register buffers (static indices only)
+  auto load = [&](float (&a)[DWH_U], float (&b)[DWH_U], int st0) {
+#pragma unroll
+    for (int u = 0; u < DWH_U; ++u) {
+      const int stp = st0 + 4 * u;
+      const int m = 2 * stp + half;
+      const int mc = min(m, M - 1);
+      const float live = (stp < se && m < M) ? 1.0f : 0.0f;
+      if (VAR & 2) {
+        a[u] = amul * (float)mc; b[u] = live;
+      } else {
+        a[u] = fmaf(S0[(int64_t)mc * S + sl], amul, aadd);
+        b[u] = dHYP[(int64_t)mc * NH + jl] * live;
+      }
+    }
+  };
+  auto mma = [&](const float (&a)[DWH_U], const float (&b)[DWH_U]) {
+#pragma unroll
+    for (int u = 0; u < DWH_U; ++u) {
+      if (VAR & 1) acc[u] = fmaf(a[u], b[u], acc[u]);
+      else acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
+    }
+  };
+  constexpr int BLK = 4 * DWH_U;   // steps per block over the four waves
+  int st = sb + wv;
+  const int nblk = (se - sb + BLK - 1) / BLK;
+  if (nblk > 0) load(a0, b0, st);
+  for (int blk = 0; blk < nblk; blk += 2) {
+    if (blk + 1 < nblk) load(a1, b1, st + BLK);
+    mma(a0, b0);
+    if (blk + 1 >= nblk) break;
+    if (blk + 2 < nblk) load(a0, b0, st + 2 * BLK);
+    mma(a1, b1);
+    st += 2 * BLK;
+  }
+  // D[i = s][j]: lane holds column j = c, rows i = 8 (r / 4) + 4 half + r % 4
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[wv][c * (DWH_T + 1) + 8 * (r >> 2) + 4 * half + (r & 3)] = acc[r];
+  __syncthreads();
+  float* out = slab + (int64_t)z * len;
+  const int64_t base = L.o[MQ_P_HW1_W];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = tid + 256 * q, jj = j0 + (e >> 5), ss = s0 + (e & 31);
+    const int o = (e >> 5) * (DWH_T + 1) + (e & 31);
+    const float v = red[0][o] + red[1][o] + red[2][o] + red[3][o];
+    if (jj < NH && ss <= S) {
+      const HypSeg sg = hyp_seg(L, d.n * d.E, d.E, jj);
+      if (ss < S) out[sg.w - base + (int64_t)sg.row * S + ss] = v;
+      else out[sg.b - base + sg.row] = v;
+    }
+  }
+}
+
+}  // namespace mq

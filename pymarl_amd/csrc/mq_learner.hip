@@ -28,6 +28,7 @@
 #include "gru_bwd_fused.hpp"
 #include "mix_kernels.hpp"
 #include "hyper_kernel.hpp"
+#include "dwh_kernel.hpp"
 #include "optim_kernels.hpp"
 
 using namespace mq;
@@ -84,6 +85,7 @@ struct mq_handle {
   bool force_unfused = getenv("MQ_UNFUSED_FWD") != nullptr;       // A/B switch for the fused agent forward
   bool force_unfused_bwd = getenv("MQ_UNFUSED_BWD") != nullptr;   // A/B switch for the fused BPTT
   bool force_unfused_mix = getenv("MQ_GEMM_HYPER") != nullptr;   // A/B switch: hypernet through gemm_f32
+  int dwh_split = getenv("MQ_DWH_SPLIT") ? atoi(getenv("MQ_DWH_SPLIT")) : 8;   // m-slices of the dW_hyper pass
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
   int slots = 0;
@@ -396,7 +398,13 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   }
   if (c.mixer == MQ_MIXER_QMIX) {
     pt.begin(PH_HYP);
-    if (hyper_ok(d.S, d.NH) && !h->force_unfused_mix) {
+    if (hyper_ws_ok(d.S, d.E, d.NH, d.M) && !h->force_unfused_mix) {
+      // wave-specialised weight streaming (hyper_kernel.hpp)
+      hipLaunchKernelGGL(hyper_ws_kernel<0>, dim3((d.M + HYR - 1) / HYR, 2), dim3(HYWS_THREADS),
+                         hyper_ws_lds_bytes(d.S), s, d, rp, (const float*)h->on, (const float*)h->tg, L, w.HYP,
+                         w.S0);
+      MQ_HIP(hipGetLastError());
+    } else if (hyper_ok(d.S, d.NH) && !h->force_unfused_mix) {
       const size_t dyn = HyperGeom(d.S, d.NH).lds_bytes();
       hipLaunchKernelGGL(hyper_kernel<0>, dim3((d.M + HYR - 1) / HYR, 2), dim3(256), dyn, s, d, rp,
                          (const float*)h->on, (const float*)h->tg, L, w.HYP, w.S0);
@@ -449,6 +457,15 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   }
   if (c.mixer == MQ_MIXER_QMIX) {
     pt.begin(PH_DWH);
+    if (!h->force_unfused_mix) {
+      // 32 x 32 output tiles x nsplit m-slices, operands straight from global memory (dwh_kernel.hpp)
+      const int tj = (d.NH + DWH_T - 1) / DWH_T, ts = (d.S + 1 + DWH_T - 1) / DWH_T;
+      const int ns = std::max(1, std::min({h->dwh_split, kNsplitMax, (d.M + 1) / 2}));
+      h->nsplit_mix = ns;
+      hipLaunchKernelGGL(dwh_kernel<0>, dim3(tj * ts * ns), dim3(256), 0, s, d, L, (const float*)w.dHYP,
+                         (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj);
+      MQ_HIP(hipGetLastError());
+    } else {
     const int tiles = ((d.NH + GBM - 1) / GBM) * ((d.S + DwhProb::BN - 1) / DwhProb::BN);
     int ns = std::max(1, std::min(kNsplitMax, std::min((512 + tiles - 1) / tiles, d.M / 64)));
     int64_t chunk = ((d.M + ns - 1) / ns + GBK - 1) / GBK * GBK;
@@ -456,6 +473,7 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
     h->nsplit_mix = ns;
     DwhProb p{d, L, w.dHYP, w.S0, w.slab_mix, h->len_mix, ns};
     MQ_HIP(launch_gemm(p, d.NH, d.S, ns, s));
+    }
   }
   pt.begin(PH_RED);
   {

@@ -1,11 +1,13 @@
 // Microbenchmark of the persistent GRU recurrence kernels at a given (B, n, T) with random data.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/rec_micro.hip -o /tmp/rec_micro && /tmp/rec_micro 32 8 120
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
 #include "../pymarl_amd/csrc/gru_bwd_fused.hpp"
 #include "../pymarl_amd/csrc/hyper_kernel.hpp"
+#include "../pymarl_amd/csrc/dwh_kernel.hpp"
 using namespace mq;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
@@ -25,6 +27,10 @@ float* dev_rand(size_t n, float scale) {
   for (auto& x : h) x = scale * ((rand() / (float)RAND_MAX) * 2.0f - 1.0f);
   float* d; CK(hipMalloc(&d, n * 4)); CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
   return d;
+}
+
+__global__ void empty_kernel(float* p) {
+  if (p && threadIdx.x == 0 && blockIdx.x == 0) p[0] = 1.0f;
 }
 
 int main(int argc, char** argv) {
@@ -185,16 +191,66 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&HYPb, (int64_t)2 * d.M * d.NH * 4)); CK(hipMalloc(&S0b, (int64_t)d.M * d.S * 4 + (1 << 20)));
     const size_t dynh = HyperGeom(d.S, d.NH).lds_bytes();
     dim3 gh((d.M + HYR - 1) / HYR, 2);
-    printf("hyper %.1f us\n", time_it([&] { hipLaunchKernelGGL(hyper_kernel<0>, gh, dim3(256), dynh, 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b); }));
-    hipLaunchKernelGGL(hyper_kernel<1>, gh, dim3(256), dynh, 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b);
+    printf("hyper %.1f us\n", time_it([&] { hipLaunchKernelGGL((hyper_kernel<0, 4>), gh, dim3(256), dynh, 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b); }));
+    {
+      const size_t nh = (size_t)2 * d.M * d.NH;
+      std::vector<float> h4(nh), h8(nh);
+      hipLaunchKernelGGL((hyper_kernel<0, 4>), gh, dim3(256), dynh, 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b);
+      CK(hipMemcpy(h4.data(), HYPb, nh * 4, hipMemcpyDeviceToHost));
+      CK(hipMemset(HYPb, 0, nh * 4));
+      hipLaunchKernelGGL((hyper_kernel<0, 8>), gh, dim3(512), dynh, 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b);
+      CK(hipMemcpy(h8.data(), HYPb, nh * 4, hipMemcpyDeviceToHost));
+      size_t bad = 0;
+      for (size_t i = 0; i < nh; ++i) bad += h4[i] != h8[i];
+      printf("hyper 4 vs 8 waves: %zu of %zu outputs differ\n", bad, nh);
+      CK(hipMemset(HYPb, 0, nh * 4));
+      hipLaunchKernelGGL(hyper_ws_kernel<0>, gh, dim3(HYWS_THREADS), hyper_ws_lds_bytes(d.S), 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b);
+      CK(hipMemcpy(h8.data(), HYPb, nh * 4, hipMemcpyDeviceToHost));
+      bad = 0;
+      double md = 0.0;
+      for (size_t i = 0; i < nh; ++i) {
+        bad += h4[i] != h8[i];
+        md = std::max(md, (double)fabsf(h4[i] - h8[i]) / (1e-3 + fabsf(h4[i])));
+      }
+      printf("hyper 4 waves vs wave-specialised: %zu of %zu outputs differ, max rel diff %.2e\n", bad, nh, md);
+    }
+    printf("hyper 8 waves %.1f us\n", time_it([&] { hipLaunchKernelGGL((hyper_kernel<0, 8>), gh, dim3(512), dynh, 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b); }));
+    printf("hyper wave-specialised %.1f us\n", time_it([&] { hipLaunchKernelGGL(hyper_ws_kernel<0>, gh, dim3(HYWS_THREADS), hyper_ws_lds_bytes(d.S), 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b); }));
+    printf("hyper wave-specialised V2(chunk-0 weights only) %.1f us\n", time_it([&] { hipLaunchKernelGGL(hyper_ws_kernel<2>, gh, dim3(HYWS_THREADS), hyper_ws_lds_bytes(d.S), 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b); }));
+    printf("hyper wave-specialised V4(no MFMA) %.1f us, V8(no staging) %.1f us, V12 %.1f us\n",
+      time_it([&] { hipLaunchKernelGGL(hyper_ws_kernel<4>, gh, dim3(HYWS_THREADS), hyper_ws_lds_bytes(d.S), 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b); }),
+      time_it([&] { hipLaunchKernelGGL(hyper_ws_kernel<8>, gh, dim3(HYWS_THREADS), hyper_ws_lds_bytes(d.S), 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b); }),
+      time_it([&] { hipLaunchKernelGGL(hyper_ws_kernel<12>, gh, dim3(HYWS_THREADS), hyper_ws_lds_bytes(d.S), 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b); }));
+    hipLaunchKernelGGL(hyper_ws_kernel<1>, gh, dim3(HYWS_THREADS), hyper_ws_lds_bytes(d.S), 0, d, rh, (const float*)P0, (const float*)P1, L, HYPb, S0b);
     CK(hipDeviceSynchronize());
     const int nb = gh.x * gh.y;
-    std::vector<uint64_t> hs(8 * nb);
+    std::vector<uint64_t> hs(32 * nb);
     CK(hipMemcpy(hs.data(), S0b, hs.size() * 8, hipMemcpyDeviceToHost));
-    double a[7] = {0, 0, 0, 0, 0, 0, 0};
-    for (int i = 0; i < nb; ++i) for (int k = 0; k < 7; ++k) a[k] += hs[8 * i + k];
-    printf("hyper stamps (cycles, mean over %d WGs): first fetch %.0f, state gather %.0f, barriers %.0f, stores %.0f, fetch %.0f, mfma+epi %.0f, total %.0f\n",
-           nb, a[0] / nb, a[1] / nb, a[2] / nb, a[3] / nb, a[4] / nb, a[5] / nb, a[6] / nb);
+    double mm[10] = {}, ll[9] = {};
+    for (int i = 0; i < nb; ++i) {
+      const uint64_t* r = &hs[32 * i];
+      for (int k = 0; k < 10; ++k) mm[k] += (double)(int64_t)(r[k] - r[0]);
+      for (int k = 0; k < 9; ++k) ll[k] += (double)(int64_t)(r[16 + k] - r[0]);
+    }
+    printf("hyper_ws stamps (cycles after the MFMA wave's start, mean over %d WGs)\n  MFMA wave: prologue done %.0f, after barrier c:", nb, mm[1] / nb);
+    for (int k = 2; k < 8; ++k) printf(" %.0f", mm[k] / nb);
+    printf(", end %.0f\n  loader   : start %.0f, at barrier c:", mm[9] / nb, ll[0] / nb);
+    for (int k = 1; k < 7; ++k) printf(" %.0f", ll[k] / nb);
+    printf(", end %.0f\n", ll[8] / nb);
+  }
+  {  // dW_hyper
+    float* dH = dev_rand((int64_t)d.M * d.NH, 1.0f);
+    float* S0d = dev_rand((int64_t)d.M * d.S, 1.0f);
+    const int64_t len = L.o[MQ_P_V2_W] - L.o[MQ_P_HW1_W];
+    float* slab; CK(hipMalloc(&slab, 128 * len * 4));
+    const int tj = (d.NH + DWH_T - 1) / DWH_T, ts = (d.S + 1 + DWH_T - 1) / DWH_T;
+    for (int nb : {1, 256, 528, 2048})
+      printf("empty kernel, %d WGs: %.1f us\n", nb, time_it([&] { hipLaunchKernelGGL(empty_kernel, dim3(nb), dim3(256), 0, 0, slab); }));
+    for (int ns : {8, 16, 32}) {
+      auto go = [&](auto k) { return time_it([&] { hipLaunchKernelGGL(k, dim3(tj * ts * ns), dim3(256), 0, 0, d, L, (const float*)dH, (const float*)S0d, slab, len, ns, tj); }); };
+      printf("dwh ns=%d: %.1f us, V1(no MFMA) %.1f, V2(no loads) %.1f, V3 %.1f\n", ns, go(dwh_kernel<0>), go(dwh_kernel<1>),
+             go(dwh_kernel<2>), go(dwh_kernel<3>));
+    }
   }
   printf("bwd RW1 %.1f us\n", runb(gru_bwd_kernel<1, 0>, 1));
   printf("bwd RW1 V4(cached inputs) %.1f us\n", runb(gru_bwd_kernel<1, 4>, 1));
