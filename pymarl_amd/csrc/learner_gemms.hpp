@@ -40,25 +40,27 @@ MQ_DEV void for_tile(const f32x16& acc, int mrow0, int ncol0, int lane, F&& f) {
 }
 
 // ---------------------------------------------------------------------------------------------- forward
+// Both nets in one pass: the B tile's 128 columns are [online W1 rows | target W1 rows] (BN = 128, grid.z = 1), so
+// each agent-input row is gathered and built once and feeds both nets' fc1.
 struct Fc1Prob {
-  static constexpr int BN = 64;
+  static constexpr int BN = 2 * H;
   Dims d;
   Rep rp;
   const float* P0;
   const float* P1;
   int64_t o_w, o_b;
   float* X1;   // [2][M][H]
-  float* XIN;  // [M][I], written by the z == 0 pass
+  float* XIN;  // [M][I], written once
   int64_t M;
   using APat = KPat;
   using BPat = KPat;
   static constexpr bool kRowSum = false;
   struct Ctx {
     const float* arow;
-    const float* brow;
+    const float* brow[2];
     int m, aprev, ag;
   };
-  MQ_DEV Ctx make_ctx(int m0, int n0, int z, int tid) const {
+  MQ_DEV Ctx make_ctx(int m0, int, int, int tid) const {
     Ctx c;
     c.m = m0 + KPat::row(tid);
     c.arow = nullptr;
@@ -73,41 +75,54 @@ struct Fc1Prob {
       // actions_onehot[t-1] is zero unless slot t-1 was filled (runner contract, synthetic.py)
       if (d.last_action && t > 0 && rp.filled[slot - 1]) c.aprev = (int)rp.actions[(slot - 1) * d.n + ag];
     }
-    const int nn = n0 + KPat::row(tid);
-    c.brow = (nn < H) ? (z ? P1 : P0) + o_w + (int64_t)nn * d.I : nullptr;
+    const int nn = KPat::row(tid);   // < H: pass p covers net p's 64 output units
+    c.brow[0] = P0 + o_w + (int64_t)nn * d.I;
+    c.brow[1] = P1 + o_w + (int64_t)nn * d.I;
     return c;
   }
   MQ_DEV void krange(int, int& kb, int& ke) const { kb = 0; ke = d.I; }
-  MQ_DEV float xin(const Ctx& c, int k) const {
-    if (k < d.O) return c.arow[k];
-    int f = k - d.O;
-    if (d.last_action) {
-      if (f < d.A) return f == c.aprev ? 1.0f : 0.0f;
-      f -= d.A;
-    }
-    return f == c.ag ? 1.0f : 0.0f;
-  }
   MQ_DEV void load_a(const Ctx& c, int k0, int ke, float (&r)[4]) const {
     const int k = k0 + KPat::kq(threadIdx.x);
+    if (c.arow && k + 3 < d.O) {   // the common case: four obs features, independent loads
 #pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = (c.arow && k + i < ke) ? xin(c, k + i) : 0.0f;
-    if (XIN && c.arow && blockIdx.z == 0 && blockIdx.y == 0) {
+      for (int i = 0; i < 4; ++i) r[i] = c.arow[k + i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int kk = k + i;
+        float v = 0.0f;
+        if (c.arow && kk < ke) {
+          if (kk < d.O) {
+            v = c.arow[kk];
+          } else {
+            int f = kk - d.O;
+            if (d.last_action) {
+              if (f < d.A) v = f == c.aprev ? 1.0f : 0.0f;
+              f -= d.A;
+            }
+            if (f >= 0 && f == c.ag) v = 1.0f;
+          }
+        }
+        r[i] = v;
+      }
+    }
+    if (XIN && c.arow) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if (k + i < ke) XIN[(int64_t)c.m * d.I + k + i] = r[i];
     }
   }
-  MQ_DEV void load_b(const Ctx& c, int, int k0, int ke, float (&r)[4]) const {
+  MQ_DEV void load_b(const Ctx& c, int pass, int k0, int ke, float (&r)[4]) const {
     const int k = k0 + KPat::kq(threadIdx.x);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = (c.brow && k + i < ke) ? c.brow[k + i] : 0.0f;
+    for (int i = 0; i < 4; ++i) r[i] = k + i < ke ? c.brow[pass][k + i] : 0.0f;
   }
-  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int z, int lane) const {
-    const int j = ncol0 + (lane & 31);
-    if (j >= H) return;
-    const float bj = (z ? P1 : P0)[o_b + j];
+  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int, int lane) const {
+    const int z = ncol0 >= H ? 1 : 0;
+    const int c0 = ncol0 - z * H;
+    const float bj = (z ? P1 : P0)[o_b + c0 + (lane & 31)];
     float* out = X1 + (int64_t)z * M * H;
-    for_tile(acc, mrow0, ncol0, lane, [&](int m, int jj, float v) {
+    for_tile(acc, mrow0, c0, lane, [&](int m, int jj, float v) {
       if (m < M) out[(int64_t)m * H + jj] = fmaxf(v + bj, 0.0f);
     });
   }

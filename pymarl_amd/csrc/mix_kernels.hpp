@@ -25,7 +25,14 @@ MQ_DEV float qmix_fwd_lane(const float* hyp, const float* qs_lds, const float* V
   float prod = 0.0f, vt = 0.0f, pre = 0.0f, hid = 0.0f, wfr = 0.0f, hv = 0.0f;
   if (lane < E) {
     float acc = 0.0f;
-    for (int ag = 0; ag < n; ++ag) acc = fmaf(qs_lds[ag], fabsf(hyp[ag * E + lane]), acc);   // bmm(q, |w1|)
+    for (int a0 = 0; a0 < n; a0 += 8) {   // bmm(q, |w1|), 8 independent loads per round trip
+      float hv8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) hv8[u] = hyp[min(a0 + u, n - 1) * E + lane];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (a0 + u < n) acc = fmaf(qs_lds[a0 + u], fabsf(hv8[u]), acc);
+    }
     pre = acc + hyp[nE + E + lane];                                                          // + b1
     hid = eluf(pre);
     wfr = hyp[nE + lane];
@@ -68,22 +75,30 @@ __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* _
     const float* qn = Qon + ((int64_t)(t + 1) * R + r) * A;
     const float* qt = Qtg + ((int64_t)(t + 1) * R + r) * A;
     const int32_t* av = rp.avail + ((slot + 1) * n + lane) * (int64_t)A;
+    // argmax over available actions, first index on ties (torch max): the row is fetched in blocks of kMB
+    // independent loads so a wave waits on ceil(A / kMB) round trips instead of A
+    const float* qsel = d.double_q ? qn : qt;
+    constexpr int kMB = 12;
+    float best = 0.0f;
     int cur = 0;
-    if (d.double_q) {
-      float best = 0.0f;
-      for (int a = 0; a < A; ++a) {
-        const float v = av[a] ? qn[a] : kNegMask;
-        if (a == 0 || v > best) { best = v; cur = a; }
+    for (int a0 = 0; a0 < A; a0 += kMB) {
+      float qv[kMB];
+      int32_t avv[kMB];
+#pragma unroll
+      for (int u = 0; u < kMB; ++u) {
+        const int a = min(a0 + u, A - 1);
+        qv[u] = qsel[a];
+        avv[u] = av[a];
       }
-      tmax = av[cur] ? qt[cur] : kNegMask;
-    } else {
-      float best = 0.0f;
-      for (int a = 0; a < A; ++a) {
-        const float v = av[a] ? qt[a] : kNegMask;
-        if (a == 0 || v > best) { best = v; cur = a; }
+#pragma unroll
+      for (int u = 0; u < kMB; ++u) {
+        const int a = a0 + u;
+        const float v = avv[u] ? qv[u] : kNegMask;
+        if (a < A && (a == 0 || v > best)) { best = v; cur = a; }
       }
-      tmax = best;
     }
+    if (d.double_q) tmax = av[cur] ? qt[cur] : kNegMask;
+    else tmax = best;
     if (curmax_out) curmax_out[(int64_t)t * R + r] = cur;
   }
   chs[wv][lane] = chosen;
@@ -128,15 +143,28 @@ __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* _
       dh[n * E + E + lane] = dpre;                                            // hyper_b_1
       dh[n * E + 2 * E + lane] = dy * V2w0[lane] * (k.hv > 0.0f ? 1.0f : 0.0f);   // V.0 (through relu)
       dv2 = dy * fmaxf(k.hv, 0.0f);                                           // V.2 weight
-      for (int ag = 0; ag < n; ++ag)                                          // hyper_w_1 (through |.|)
-        dh[ag * E + lane] = (chs[wv][ag] * dpre) * sgnf(hon[ag * E + lane]);
+      for (int a0 = 0; a0 < n; a0 += 8) {                                     // hyper_w_1 (through |.|)
+        float hv8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) hv8[u] = hon[min(a0 + u, n - 1) * E + lane];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (a0 + u < n) dh[(a0 + u) * E + lane] = (chs[wv][a0 + u] * dpre) * sgnf(hv8[u]);
+      }
     }
     dv2b = dy;
     dps[wv][lane] = dpre;
     __syncthreads();
     if (valid && lane < n) {
       float acc = 0.0f;
-      for (int e = 0; e < E; ++e) acc = fmaf(fabsf(hon[lane * E + e]), dps[wv][e], acc);
+      for (int e0 = 0; e0 < E; e0 += 8) {
+        float hv8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) hv8[u] = hon[lane * E + min(e0 + u, E - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (e0 + u < E) acc = fmaf(fabsf(hv8[u]), dps[wv][e0 + u], acc);
+      }
       w.dch[(int64_t)t * R + b * n + lane] = acc;
     }
   } else {

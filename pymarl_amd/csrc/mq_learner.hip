@@ -375,7 +375,7 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
     pt.begin(PH_FC1);
     {
       Fc1Prob p{d, rp, h->on, h->tg, h->off[MQ_P_FC1_W], h->off[MQ_P_FC1_B], w.X1, w.XIN, RT};
-      MQ_HIP(launch_gemm(p, (int)RT, mq::H, 2, s));
+      MQ_HIP(launch_gemm(p, (int)RT, 2 * mq::H, 1, s));
     }
     pt.begin(PH_GI);
     {

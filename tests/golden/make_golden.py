@@ -179,7 +179,8 @@ def run_case(name, case):
     np.random.seed(case["sampler_seed"])
     out = {k: np.array(v) for k, v in case.items() if not isinstance(v, str)}
     out["mixer"] = np.array(case["mixer"])
-    out["params_init"] = flat_params(learner)
+    if case.get("store_params", True):
+        out["params_init"] = flat_params(learner)
     ids_all, losses, full = [], [], case["full"]
     cur_max_steps, margin_steps = [], []
     per_step = {"params": [], "targets": [], "sqavg": []}
@@ -232,7 +233,7 @@ def run_case(name, case):
         out["step_params"] = np.stack(per_step["params"])
         out["targets_final"] = per_step["targets"][-1]
         out["sqavg_final"] = per_step["sqavg"][-1]
-    else:
+    elif case.get("store_params", True):
         out["params_final"] = flat_params(learner)
         out["targets_final"] = flat_targets(learner)
     path = os.path.join(HERE, name + ".npz")
@@ -247,6 +248,11 @@ CFG2 = dict(n=8, A=14, O=80, S=168, T=120, B=32, n_episodes=64, data_seed=0, wei
             ragged=False, steps=20, episodes=[8 * k for k in range(10)] + [200 + 8 * k for k in range(10)],
             full=False, record_actions_steps=3)
 
+CFG3 = dict(n=27, A=36, O=285, S=1170, T=180, B=4, n_episodes=8, data_seed=0, weight_seed=1, sampler_seed=2,
+            ragged=True, steps=4, episodes=[0, 8, 200, 208], full=False, record_actions_steps=2)
+CFG4 = dict(n=5, A=11, O=80, S=120, T=120, B=64, n_episodes=96, data_seed=0, weight_seed=1, sampler_seed=2,
+            ragged=False, steps=4, episodes=[0, 8, 200, 208], full=False, record_actions_steps=2)
+
 CASES = {
     "tiny_qmix": dict(TINY, mixer="qmix"),
     "tiny_vdn": dict(TINY, mixer="vdn"),
@@ -254,6 +260,12 @@ CASES = {
     "cfg2_qmix": dict(CFG2, mixer="qmix"),
     "cfg2_vdn": dict(CFG2, mixer="vdn", steps=10, episodes=[8 * k for k in range(5)] + [200 + k for k in range(5)]),
     "cfg2_qmix_ragged": dict(CFG2, mixer="qmix", ragged=True, steps=5, episodes=[0, 8, 200, 208, 216]),
+    # BASELINE configs[2] shape (27m_vs_30m, VDN) at a reduced batch: A=36 > 16 and I=348 run the unfused kernels
+    "cfg3_vdn": dict(CFG3, mixer="vdn"),
+    # the same shape under QMIX: S=1170 exercises the hypernet / dW_hyper kernels at a long K
+    "cfg3_qmix": dict(CFG3, mixer="qmix", steps=3, episodes=[0, 8, 200], store_params=False),
+    # BASELINE configs[3] shape (2s3z, QMIX): one rank's shard of B=512 over 8 GPUs, R = 64*5 = 320 rows > 256
+    "cfg4_qmix": dict(CFG4, mixer="qmix"),
 }
 
 if __name__ == "__main__":

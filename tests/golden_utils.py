@@ -9,7 +9,8 @@ import numpy as np
 from pymarl_amd.utils.synthetic import agent_param_shapes, init_params, make_replay, qmix_param_shapes
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASE_NAMES = ["tiny_qmix", "tiny_vdn", "tiny_qmix_full", "cfg2_qmix", "cfg2_vdn", "cfg2_qmix_ragged"]
+CASE_NAMES = ["tiny_qmix", "tiny_vdn", "tiny_qmix_full", "cfg2_qmix", "cfg2_vdn", "cfg2_qmix_ragged",
+              "cfg3_vdn", "cfg3_qmix", "cfg4_qmix"]
 
 
 class Case:

@@ -89,7 +89,7 @@ def test_tiny_full(cases, name):
     run_case(get_case(cases, name), check_full=True)
 
 
-@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_vdn", "cfg2_qmix_ragged"])
+@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_vdn", "cfg2_qmix_ragged", "cfg3_vdn", "cfg3_qmix", "cfg4_qmix"])
 def test_cfg2_trajectory(cases, name):
     run_case(get_case(cases, name), check_full=False)
 
@@ -130,12 +130,25 @@ def set_state_from_oracle(learner, o):
         learner._sq.copy_(th.from_numpy(o.flat("sq")))
 
 
-@pytest.mark.parametrize("name,steps", [("cfg2_qmix", 20), ("cfg2_vdn", 10), ("cfg2_qmix_ragged", 5),
-                                        ("tiny_qmix", 4), ("tiny_vdn", 4)])
-def test_teacher_forced_steps(cases, name, steps):
+UNFUSED_ENV = ("MQ_UNFUSED_FWD", "MQ_UNFUSED_BWD", "MQ_GEMM_HYPER")
+
+
+@pytest.mark.parametrize("name,steps,unfused", [
+    ("cfg2_qmix", 20, False), ("cfg2_vdn", 10, False), ("cfg2_qmix_ragged", 5, False), ("tiny_qmix", 4, False),
+    ("tiny_vdn", 4, False),
+    # BASELINE configs[2] / configs[3] shapes: the row-batched (unfused) recurrences and the GEMM path run here
+    ("cfg3_vdn", 4, False), ("cfg3_qmix", 3, False), ("cfg4_qmix", 4, False),
+    # the A/B switches: the unfused kernel sequence on the shapes the fused kernels normally take
+    ("cfg2_qmix", 4, True), ("cfg2_qmix_ragged", 3, True), ("tiny_vdn", 2, True)])
+def test_teacher_forced_steps(cases, name, steps, unfused, monkeypatch):
     from oracle.qlearner_np import OracleQLearner, fc1_preacts
     from tests.gpu_helpers import build, flat_grads, flat_params, rel
     case = get_case(cases, name)
+    for k in UNFUSED_ENV:   # read once, at handle creation (mq_create)
+        if unfused:
+            monkeypatch.setenv(k, "1")
+        else:
+            monkeypatch.delenv(k, raising=False)
     args, buf, mac, learner, logger = build(case)
     o = OracleQLearner(case.agent_params, case.mixer_params, case.cfg())
     np.random.seed(case.sampler_seed)
@@ -144,6 +157,7 @@ def test_teacher_forced_steps(cases, name, steps):
         batch = batch[:, :batch.max_t_filled()]
         nb, _ = case.batch(k)
         set_state_from_oracle(learner, o)
+        p_prev, sq_prev = o.flat("params").astype(np.float64), o.flat("sq").astype(np.float64)
         fw = o.forward(nb)
         learner.train(batch, 1000 * k, case.episodes[k])
         st = learner.last_stats()
@@ -164,8 +178,17 @@ def test_teacher_forced_steps(cases, name, steps):
         for s_ in STATS:
             assert abs(st[s_] - st_o[s_]) <= 1e-5 * abs(st_o[s_]) + 1e-6, (name, k, s_, st[s_], st_o[s_])
         g_or = np.concatenate([v.ravel() for v in o.last["grads"].values()])
-        assert rel(flat_grads(learner), g_or) < 1e-4, (name, k)
-        assert rel(flat_params(learner), o.flat("params")) < 1e-5, (name, k)
+        g_gpu = flat_grads(learner)
+        assert rel(g_gpu, g_or) < 1e-4, (name, k)
+        # RMSprop (q_learner.py:30, torch.optim.RMSprop) on the GPU's own clipped gradient: exact up to rounding.
+        # Against the oracle's parameters only an O(lr) band holds: the per-element 1/(sqrt(v)+eps) normalisation
+        # turns a 1e-4-of-max gradient difference on a tiny-|g| element into an O(lr) step difference.
+        g64 = g_gpu.astype(np.float64)
+        sq_exp = 0.99 * sq_prev + 0.01 * g64 * g64
+        p_exp = p_prev - 5e-4 * g64 / (np.sqrt(sq_exp) + 1e-5)
+        assert rel(learner._sq.cpu().numpy(), sq_exp) < 1e-5, (name, k)
+        assert rel(flat_params(learner), p_exp) < 1e-6, (name, k)
+        assert np.abs(flat_params(learner) - o.flat("params")).max() <= 20 * 5e-4, (name, k)
 
 
 def test_data_parallel_norm_path_single_rank(cases):

@@ -43,7 +43,7 @@ def test_intermediates_and_params(golden_cases, name):
     assert rel_err(o.flat("targets"), c.z["targets_final"]) < 5e-5
 
 
-@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_vdn"])
+@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_vdn", "cfg3_vdn", "cfg3_qmix", "cfg4_qmix"])
 def test_cfg2_trajectory(golden_cases, name):
     c = golden_cases[name]
     o = OracleQLearner(c.agent_params, c.mixer_params, c.cfg())
