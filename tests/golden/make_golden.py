@@ -26,7 +26,9 @@ import os
 import sys
 from types import SimpleNamespace as SN
 
-import numpy as np
+sys.dont_write_bytecode = True   # /root/reference is read-only: no __pycache__ there
+
+import numpy as np  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))

@@ -59,3 +59,46 @@ def rel_err(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.abs(a - b).max() / max(1e-30, np.abs(b).max()))
+
+
+COMA_CASE_NAMES = ["coma_tiny", "coma_tiny_masked", "coma_cfg5"]
+COMA_STATS = ["critic_loss", "critic_grad_norm", "td_error_abs", "q_taken_mean", "target_mean", "advantage_mean",
+              "coma_loss", "agent_grad_norm", "pi_max"]
+
+
+class ComaCase:
+    """A golden COMA case (tests/golden/make_golden_coma.py): replay, weights, sampler ids, per-step epsilon."""
+
+    def __init__(self, name):
+        from oracle.coma_np import critic_input_dim, critic_param_shapes
+        self.name = name
+        z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+        self.z = {k: z[k] for k in z.files}
+        g = lambda k: int(self.z[k])  # noqa: E731
+        self.n, self.A, self.O, self.S, self.T = g("n"), g("A"), g("O"), g("S"), g("T")
+        self.B, self.n_episodes, self.steps = g("B"), g("n_episodes"), g("steps")
+        self.ragged = bool(self.z["ragged"])
+        self.mask_before_softmax = bool(self.z["mask_before_softmax"])
+        self.target_update_interval = g("target_update_interval")
+        self.data = make_replay(self.n_episodes, self.T, self.n, self.A, self.O, self.S, seed=g("data_seed"),
+                                ragged=self.ragged)
+        self.I = self.O + self.A + self.n
+        self.K = critic_input_dim(self.n, self.A, self.O, self.S)
+        self.agent_shapes = agent_param_shapes(self.I, 64, self.A)
+        self.critic_shapes = critic_param_shapes(self.K, self.A)
+        self.agent_params = init_params(self.agent_shapes, seed=g("weight_seed"))
+        self.critic_params = init_params(self.critic_shapes, seed=g("weight_seed") + 200)
+        self.sampler_seed = g("sampler_seed")
+        self.epsilon = [float(e) for e in self.z["epsilon"]]
+
+    def cfg(self):
+        return dict(n_agents=self.n, n_actions=self.A, gamma=0.99, td_lambda=0.8, lr=5e-4, critic_lr=5e-4,
+                    optim_alpha=0.99, optim_eps=1e-5, grad_norm_clip=10.0,
+                    target_update_interval=self.target_update_interval,
+                    mask_before_softmax=self.mask_before_softmax)
+
+    def batch(self, step):
+        ids = self.z["ids"][step]
+        b = OrderedDict((k, v[ids]) for k, v in self.data.items())
+        max_t = int(b["filled"].sum(1).max())
+        return OrderedDict((k, v[:, :max_t]) for k, v in b.items()), ids
