@@ -43,6 +43,9 @@ CONFIGS = {
     "cfg2": ("qmix", 8, 14, 80, 168, 120, 32, "QMIX synthetic replay n_agents=8 T=120 obs=80 state=168 batch=32"),
     "cfg3": ("vdn", 27, 36, 285, 1170, 180, 128, "VDN synthetic 27m_vs_30m shape n_agents=27 T=180 batch=128"),
     "cfg4": ("qmix", 5, 11, 80, 120, 120, 64, "QMIX 2s3z shape, 64 episodes per GPU (512 over 8 GPUs)"),
+    # COMALearner; coma_smac.yaml batch_size 8
+    "cfg5": ("coma", 10, 18, 176, 322, 180, 8, "COMA critic counterfactual baseline, MMM2 shape n_agents=10 "
+                                               "n_actions=18 T=180 batch=8"),
 }
 
 
@@ -114,6 +117,47 @@ def build_workload(cfg_name, device, n_episodes=5000, unique=512, seed=0):
     learner = le_REGISTRY["q_learner"](mac, buf.scheme, Logger(logging.getLogger("bench")), args)
     learner.cuda()
     return args, buf, learner, data
+
+
+def build_coma_workload(cfg_name, device, n_episodes=1000, unique=128, seed=0):
+    """COMALearner on an HBM-resident synthetic replay (coma_smac.yaml hyper-parameters)."""
+    import torch as th
+    from pymarl_amd.components.episode_buffer import ReplayBuffer
+    from pymarl_amd.components.transforms import OneHot
+    from pymarl_amd.controllers import REGISTRY as mac_REGISTRY
+    from pymarl_amd.learners import REGISTRY as le_REGISTRY
+    from pymarl_amd.utils.logging import Logger
+    from pymarl_amd.utils.synthetic import make_replay
+
+    _, n, A, O, S, T, B, _ = CONFIGS[cfg_name]
+    args = SN(n_agents=n, n_actions=A, state_shape=S, obs_shape=O, rnn_hidden_dim=64, lr=5e-4, critic_lr=5e-4,
+              optim_alpha=0.99, optim_eps=1e-5, grad_norm_clip=10.0, gamma=0.99, td_lambda=0.8,
+              target_update_interval=200, learner_log_interval=10 ** 12, obs_last_action=True, obs_agent_id=True,
+              agent="rnn", mac="basic_mac", agent_output_type="pi_logits", action_selector="multinomial",
+              epsilon_start=0.5, epsilon_finish=0.01, epsilon_anneal_time=100000, mask_before_softmax=False,
+              batch_size=B, learner="coma_learner", device=str(device), use_cuda=True)
+    scheme = {
+        "state": {"vshape": S},
+        "obs": {"vshape": O, "group": "agents"},
+        "actions": {"vshape": (1,), "group": "agents", "dtype": th.long},
+        "avail_actions": {"vshape": (A,), "group": "agents", "dtype": th.int},
+        "reward": {"vshape": (1,)},
+        "terminated": {"vshape": (1,), "dtype": th.uint8},
+    }
+    groups = {"agents": n}
+    buf = ReplayBuffer(scheme, groups, n_episodes, T + 1, preprocess={"actions": ("actions_onehot", [OneHot(A)])},
+                       device=device)
+    data = make_replay(unique, T, n, A, O, S, seed=seed)
+    for start in range(0, n_episodes, unique):
+        m = min(unique, n_episodes - start)
+        for k, v in data.items():
+            buf.data.transition_data[k][start:start + m] = th.as_tensor(v[:m], device=device)
+    buf.episode_lengths[:] = buf.data.transition_data["filled"].sum(1).reshape(-1).cpu().numpy()
+    buf.episodes_in_buffer = n_episodes
+    mac = mac_REGISTRY["basic_mac"](buf.scheme, groups, args)
+    learner = le_REGISTRY["coma_learner"](mac, buf.scheme, Logger(logging.getLogger("bench")), args)
+    learner.cuda()
+    return args, buf, learner, data, mac
 
 
 def cpu_baseline(cfg_name, data, budget_s=12.0):

@@ -1,0 +1,69 @@
+/* C ABI of the MI355X-native COMA learner step (libmq_learner.so, gfx950) — SURVEY.md §8f row f1.
+ *
+ * The drop-in boundary behind pymarl's learners.REGISTRY["coma_learner"]: the host shim
+ * pymarl_amd/learners/coma_learner.py binds these symbols with ctypes. Conventions as include/mq_learner.h:
+ * DEVICE pointers owned by the caller, asynchronous on the given HIP stream, int status + mq_last_error().
+ *
+ * Reference interfaces replaced (nicholasburden/pymarl, /root/reference):
+ *   mc_train_step      COMALearner.train(batch, t_env, episode_num) minus the target-update decision
+ *                      src/learners/coma_learner.py:32-98, with _train_critic :100-148, COMACritic
+ *                      src/modules/critics/coma.py:22-58, build_td_lambda_targets src/utils/rl_utils.py:4-14 and
+ *                      BasicMAC.forward's pi_logits branch src/controllers/basic_controller.py:53-73
+ *   mc_update_targets  COMALearner._update_targets                       src/learners/coma_learner.py:150-152
+ *   mc_policy          BasicMAC.forward pi_logits post-processing        src/controllers/basic_controller.py:53-73
+ *   mc_copy_intermediate  (test hook) the critic's per-step Q values, the TD(lambda) targets, the policy
+ */
+#ifndef MC_COMA_H
+#define MC_COMA_H
+
+#include "mq_learner.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { MC_CRITIC_HIDDEN = 128 };   /* coma.py:17-19 */
+/* Critic parameter tensors in COMACritic.parameters() order (coma.py:17-19). */
+enum { MC_P_FC1_W, MC_P_FC1_B, MC_P_FC2_W, MC_P_FC2_B, MC_P_FC3_W, MC_P_FC3_B, MC_P_COUNT };
+enum { MC_NTAIL = 8 };    /* tail of the critic gradient buffer (sum of the mask of the pending step ...) */
+/* stats[MC_NSTATS]: critic_loss, critic_grad_norm, td_error_abs, q_taken_mean, target_mean (means over the
+ * logged critic steps, coma_learner.py:85-88), advantage_mean, coma_loss, agent_grad_norm, pi_max (:90-93),
+ * critic training steps taken, agent mask sum; [11..15] scratch. */
+enum { MC_NSTATS = 16 };
+
+typedef struct mc_config {
+  int32_t n_agents, n_actions, obs_dim, state_dim;
+  int32_t rnn_hidden_dim;          /* 64 */
+  int32_t obs_last_action, obs_agent_id;
+  int32_t mask_before_softmax;     /* basic_controller.py:56 (getattr default True; coma_smac.yaml: False) */
+  float gamma, td_lambda, lr, critic_lr, optim_alpha, optim_eps, grad_norm_clip;
+  int32_t max_batch, max_seq;
+} mc_config;
+
+typedef struct mc_handle mc_handle;
+
+int mc_create(const mc_config* cfg, mc_handle** out);
+int mc_destroy(mc_handle* h);
+/* agent_offsets[MQ_P_COUNT + 1] (RNNAgent layout, mixer entries empty), critic_offsets[MC_P_COUNT + 1]. */
+int mc_param_offsets(const mc_handle* h, int64_t* agent_offsets, int64_t* critic_offsets);
+/* agent / agent_sq: [Pa]; agent_grad: [Pa + MQ_NSUMS]; critic / target_critic / critic_sq: [Pc];
+ * critic_grad: [Pc + MC_NTAIL]; stats: [MC_NSTATS]. Clipped gradients of the agent step and of the last critic
+ * step are left in the grad buffers, as .grad holds them after the reference's train(). */
+int mc_bind(mc_handle* h, float* agent, float* agent_grad, float* agent_sq, float* critic, float* target_critic,
+            float* critic_grad, float* critic_sq, float* stats);
+/* One COMALearner.train on `batch` (t_len = max_t_filled): T = t_len - 1 critic RMSprop steps in reversed t, the
+ * policy-gradient agent step, stats. epsilon = the MAC's action_selector.epsilon (the reference reads it through
+ * BasicMAC.forward, basic_controller.py:64-67). The caller reads stats[9] (critic steps) for the target update. */
+int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* stream);
+int mc_update_targets(mc_handle* h, void* stream);
+/* BasicMAC.forward's pi_logits branch on logits [rows][n_actions] in place: optional -1e10 mask, softmax, and
+ * unless test_mode the epsilon floor (+ zeroing when mask_before_softmax). avail [rows][n_actions] int32. */
+int mc_policy(float* logits, const int32_t* avail, int32_t rows, int32_t n_actions, float epsilon,
+              int32_t mask_before_softmax, int32_t test_mode, void* stream);
+/* 0 = critic Q values the actor used [T][B*n][A]; 1 = TD(lambda) targets [T][B*n]; 2 = policy pi [T][B*n][A]. */
+int mc_copy_intermediate(mc_handle* h, int which, float* dst, int64_t* count, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MC_COMA_H */

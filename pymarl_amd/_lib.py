@@ -26,7 +26,16 @@ EXPORTS = [
     "mq_last_error", "mq_create", "mq_destroy", "mq_param_offsets", "mq_bind", "mq_forward_backward", "mq_apply",
     "mq_train_step", "mq_update_targets", "mq_copy_intermediate", "mq_mac_forward", "mq_agent_forward",
     "mq_greedy_actions", "mq_set_timing", "mq_phase_times", "mq_phase_names", "mq_set_data_parallel",
+    # include/mc_coma.h
+    "mc_create", "mc_destroy", "mc_param_offsets", "mc_bind", "mc_train_step", "mc_update_targets", "mc_policy",
+    "mc_copy_intermediate",
 ]
+
+MC_P_COUNT = 6
+MC_NTAIL = 8
+MC_NSTATS = 16
+COMA_STATS = ["critic_loss", "critic_grad_norm", "td_error_abs", "q_taken_mean", "target_mean", "advantage_mean",
+              "coma_loss", "agent_grad_norm", "pi_max", "critic_steps", "mask_sum"]
 
 
 class MQConfig(ctypes.Structure):
@@ -47,6 +56,17 @@ class MQReplay(ctypes.Structure):
         ("filled", ctypes.c_void_p), ("ep_ids", ctypes.c_void_p), ("n_episodes", ctypes.c_int64),
         ("batch_size", ctypes.c_int32), ("t_len", ctypes.c_int32), ("t_stride", ctypes.c_int32),
         ("ep_ids_host", ctypes.c_void_p),
+    ]
+
+
+class MCConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_agents", ctypes.c_int32), ("n_actions", ctypes.c_int32), ("obs_dim", ctypes.c_int32),
+        ("state_dim", ctypes.c_int32), ("rnn_hidden_dim", ctypes.c_int32), ("obs_last_action", ctypes.c_int32),
+        ("obs_agent_id", ctypes.c_int32), ("mask_before_softmax", ctypes.c_int32), ("gamma", ctypes.c_float),
+        ("td_lambda", ctypes.c_float), ("lr", ctypes.c_float), ("critic_lr", ctypes.c_float),
+        ("optim_alpha", ctypes.c_float), ("optim_eps", ctypes.c_float), ("grad_norm_clip", ctypes.c_float),
+        ("max_batch", ctypes.c_int32), ("max_seq", ctypes.c_int32),
     ]
 
 
@@ -90,6 +110,14 @@ def load(required=True):
         "mq_set_timing": ([vp, i32, ctypes.c_uint32], ctypes.c_int),
         "mq_set_data_parallel": ([vp, i32], ctypes.c_int),
         "mq_phase_times": ([vp, ctypes.POINTER(ctypes.c_float), i32, ctypes.POINTER(i32)], ctypes.c_int),
+        "mc_create": ([ctypes.POINTER(MCConfig), ctypes.POINTER(vp)], ctypes.c_int),
+        "mc_destroy": ([vp], ctypes.c_int),
+        "mc_param_offsets": ([vp, ctypes.POINTER(i64), ctypes.POINTER(i64)], ctypes.c_int),
+        "mc_bind": ([vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
+        "mc_train_step": ([vp, ctypes.POINTER(MQReplay), ctypes.c_float, vp], ctypes.c_int),
+        "mc_update_targets": ([vp, vp], ctypes.c_int),
+        "mc_policy": ([vp, vp, i32, i32, ctypes.c_float, i32, i32, vp], ctypes.c_int),
+        "mc_copy_intermediate": ([vp, ctypes.c_int, vp, ctypes.POINTER(i64), vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -150,3 +178,27 @@ class Handle:
     @property
     def n_params(self):
         return self.offsets[-1]
+
+
+class ComaHandle:
+    """RAII owner of an mc_handle (include/mc_coma.h)."""
+
+    def __init__(self, cfg: MCConfig):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        check(self.lib.mc_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+        self.cfg = cfg
+        ao = (ctypes.c_int64 * (P_COUNT + 1))()
+        co = (ctypes.c_int64 * (MC_P_COUNT + 1))()
+        check(self.lib.mc_param_offsets(self.h, ao, co))
+        self.agent_offsets = list(ao)
+        self.critic_offsets = list(co)
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) and self.h.value:
+                self.lib.mc_destroy(self.h)
+                self.h = ctypes.c_void_p()
+        except Exception:
+            pass

@@ -2,7 +2,8 @@
 
 `forward(ep_batch, t)` is one fused HIP step (`mq_mac_forward`): it builds [obs_t | onehot(a_{t-1}) | onehot(id)]
 from the replay rows in-kernel (basic_controller.py:100-135) and runs fc1 -> GRUCell -> fc2 for every
-(episode, agent) row. Only the "q" agent_output_type (QMIX/VDN/IQL) is implemented.
+(episode, agent) row. For agent_output_type "pi_logits" (COMA) a second HIP kernel (`mc_policy`) applies the
+reference's -1e10 mask, softmax and epsilon floor in place (basic_controller.py:53-73).
 """
 import torch as th
 
@@ -27,8 +28,8 @@ class BasicMAC:
         return self.action_selector.select_action(agent_outputs[bs], avail_actions[bs], t_env, test_mode=test_mode)
 
     def forward(self, ep_batch, t, test_mode=False):
-        if self.agent_output_type != "q":
-            raise NotImplementedError("agent_output_type {!r}: only 'q' is implemented".format(self.agent_output_type))
+        if self.agent_output_type not in ("q", "pi_logits"):
+            raise NotImplementedError("agent_output_type {!r}".format(self.agent_output_type))
         from ..learners.q_learner import replay_view
         rep, keep = replay_view(ep_batch)
         bs = ep_batch.batch_size
@@ -41,6 +42,12 @@ class BasicMAC:
         _lib.check(hd.lib.mq_mac_forward(hd.h, rep, int(t), _lib.ptr(h_in), _lib.ptr(h_out), _lib.ptr(q), 0,
                                          _lib.stream_ptr()))
         self.hidden_states = h_out.view(bs, self.n_agents, H)
+        if self.agent_output_type == "pi_logits":
+            avail = ep_batch["avail_actions"][:, t].to(dtype=th.int32).contiguous()
+            eps = float(self.action_selector.epsilon)
+            _lib.check(hd.lib.mc_policy(_lib.ptr(q), _lib.ptr(avail), q.shape[0], q.shape[1], eps,
+                                        int(bool(getattr(self.args, "mask_before_softmax", True))),
+                                        int(bool(test_mode)), _lib.stream_ptr()))
         return q.view(bs, self.n_agents, -1)
 
     def init_hidden(self, batch_size):

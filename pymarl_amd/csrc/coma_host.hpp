@@ -1,0 +1,344 @@
+// Host side of the COMA learner step (include/mc_coma.h), included at the end of mq_learner.hip so it shares the
+// QMIX learner's error handling, replay plumbing and agent kernels. The agent (RNNAgent) forward / BPTT reuses an
+// internal mq_handle (no mixer) for its workspace; the critic has its own.
+#include "../../include/mc_coma.h"
+#include "coma_kernels.hpp"
+
+struct mc_handle {
+  mc_config cfg;
+  mq_handle* ah = nullptr;   // agent workspace + kernels
+  int I, Kc, Kp, Ap;
+  int64_t aoff[MQ_P_COUNT + 1];
+  int64_t coff[MC_P_COUNT + 1];
+  int64_t Pa, Pc;
+  float *agent = nullptr, *agrad = nullptr, *asq = nullptr, *critic = nullptr, *tcritic = nullptr,
+        *cgrad = nullptr, *csq = nullptr, *stats = nullptr;
+  void* ws = nullptr;
+  // critic workspace
+  float *X, *H1t, *H2t, *Qt, *tgt, *msum, *H1c, *H2c, *dH1c, *dH2c, *dqc, *qvals, *cpart, *cnorm, *crec;
+  float *Pshadow, *SQshadow;
+  int* actc;
+  int* cstate;
+  // actor workspace
+  float *dL, *dHo, *pi, *ppart, *slab_fc2, *red_tmp, *norm_part;
+  int last_T = 0, last_R = 0;
+};
+
+namespace {
+
+int mc_agent_config(const mc_config& c, mq_config* a) {
+  std::memset(a, 0, sizeof(*a));
+  a->n_agents = c.n_agents; a->n_actions = c.n_actions; a->obs_dim = c.obs_dim; a->state_dim = c.state_dim;
+  a->rnn_hidden_dim = c.rnn_hidden_dim; a->mixing_embed_dim = 0; a->mixer = MQ_MIXER_NONE; a->double_q = 0;
+  a->obs_last_action = c.obs_last_action; a->obs_agent_id = c.obs_agent_id; a->gamma = c.gamma; a->lr = c.lr;
+  a->optim_alpha = c.optim_alpha; a->optim_eps = c.optim_eps; a->grad_norm_clip = c.grad_norm_clip;
+  a->max_batch = c.max_batch; a->max_seq = c.max_seq;
+  return MQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mc_create(const mc_config* cfg, mc_handle** out) {
+  if (!cfg || !out) return set_err(MQ_ERR_ARG, "NULL argument");
+  const mc_config& c = *cfg;
+  if (c.n_actions < 1 || c.n_actions > 64) return set_err(MQ_ERR_ARG, "n_actions must be in [1, 64]");
+  if (c.max_batch * c.n_agents > MQ_INLINE_IDS * 64) return set_err(MQ_ERR_ARG, "max_batch * n_agents too large");
+  mq_config ac;
+  mc_agent_config(c, &ac);
+  mq_handle* ah = nullptr;
+  int rc = mq_create(&ac, &ah);
+  if (rc) return rc;
+  mc_handle* h = new mc_handle();
+  h->cfg = c;
+  h->ah = ah;
+  h->I = ah->I;
+  for (int i = 0; i <= MQ_P_COUNT; ++i) h->aoff[i] = ah->off[i];
+  h->Pa = ah->P;
+  const int n = c.n_agents, A = c.n_actions;
+  h->Kc = c.state_dim + c.obs_dim + 2 * n * A + n;   // coma.py:61-70
+  h->Kp = (h->Kc + 3) & ~3;
+  h->Ap = (A + 3) & ~3;
+  const int64_t sz[MC_P_COUNT] = {(int64_t)CH * h->Kc, CH, (int64_t)CH * CH, CH, (int64_t)A * CH, A};
+  int64_t o = 0;
+  for (int i = 0; i < MC_P_COUNT; ++i) { h->coff[i] = o; o += sz[i]; }
+  h->coff[MC_P_COUNT] = o;
+  h->Pc = o;
+
+  const int64_t Tp = c.max_seq, R = (int64_t)c.max_batch * n, T = Tp - 1;
+  const int64_t RTa = T * R;   // actor rows (T steps)
+  const int64_t nwg = 8 * ((h->Kc + 1 + 63) / 64) + 24 + 3 * ((A + 15) / 16) + 1, nhead = (R + 15) / 16;
+  const int64_t ns2 = kNsplitMax;
+  const int64_t red_tmp = kRedZ * ((int64_t)mq::H * h->I + mq::H) + kRedZ * h->ah->len_rnn +
+                          kRedZ * (A * mq::H + A) + kRedZ * 8;
+  int64_t sizes[] = {
+      Tp * R * h->Kp,              // X
+      Tp * R * CH, Tp * R * CH,    // H1t, H2t
+      Tp * R * A,                  // Qt
+      T * R, T,                    // tgt, msum
+      R * CH, R * CH, R * CH, R * CH,   // H1c H2c dH1c dH2c
+      R, R,                        // dqc, actc
+      T * R * A,                   // qvals
+      nhead * 8, nwg, T * 8,       // cpart, cnorm, crec
+      h->Pc, h->Pc,                // shadow params / square_avg
+      4,                           // cstate
+      RTa * h->Ap, RTa * mq::H, RTa * A,   // dL, dHo, pi
+      ((RTa + 3) / 4) * 8,         // ppart
+      ns2 * (A * mq::H + A),       // slab_fc2
+      red_tmp,                     // red_tmp
+      4096,                        // norm_part
+  };
+  const int NS = (int)(sizeof(sizes) / sizeof(sizes[0]));
+  int64_t total = 0, offs[32];
+  for (int i = 0; i < NS; ++i) { offs[i] = total; total += align_up(std::max<int64_t>(sizes[i], 1)); }
+  hipError_t e = hipMalloc(&h->ws, total * sizeof(float));
+  if (e != hipSuccess) {
+    mq_destroy(ah);
+    delete h;
+    return set_err(MQ_ERR_HIP, std::string("COMA workspace hipMalloc: ") + hipGetErrorString(e));
+  }
+  float* b = (float*)h->ws;
+  int k = 0;
+  h->X = b + offs[k++]; h->H1t = b + offs[k++]; h->H2t = b + offs[k++]; h->Qt = b + offs[k++];
+  h->tgt = b + offs[k++]; h->msum = b + offs[k++];
+  h->H1c = b + offs[k++]; h->H2c = b + offs[k++]; h->dH1c = b + offs[k++]; h->dH2c = b + offs[k++];
+  h->dqc = b + offs[k++]; h->actc = (int*)(b + offs[k++]);
+  h->qvals = b + offs[k++]; h->cpart = b + offs[k++]; h->cnorm = b + offs[k++]; h->crec = b + offs[k++];
+  h->Pshadow = b + offs[k++]; h->SQshadow = b + offs[k++];
+  h->cstate = (int*)(b + offs[k++]);
+  h->dL = b + offs[k++]; h->dHo = b + offs[k++]; h->pi = b + offs[k++]; h->ppart = b + offs[k++];
+  h->slab_fc2 = b + offs[k++]; h->red_tmp = b + offs[k++]; h->norm_part = b + offs[k++];
+  *out = h;
+  return MQ_OK;
+}
+
+int mc_destroy(mc_handle* h) {
+  if (!h) return MQ_OK;
+  if (h->ws) (void)hipFree(h->ws);
+  mq_destroy(h->ah);
+  delete h;
+  return MQ_OK;
+}
+
+int mc_param_offsets(const mc_handle* h, int64_t* agent_offsets, int64_t* critic_offsets) {
+  if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
+  if (agent_offsets)
+    for (int i = 0; i <= MQ_P_COUNT; ++i) agent_offsets[i] = h->aoff[i];
+  if (critic_offsets)
+    for (int i = 0; i <= MC_P_COUNT; ++i) critic_offsets[i] = h->coff[i];
+  return MQ_OK;
+}
+
+int mc_bind(mc_handle* h, float* agent, float* agent_grad, float* agent_sq, float* critic, float* target_critic,
+            float* critic_grad, float* critic_sq, float* stats) {
+  if (!h || !agent || !agent_grad || !agent_sq || !critic || !target_critic || !critic_grad || !critic_sq || !stats)
+    return set_err(MQ_ERR_ARG, "mc_bind: NULL pointer");
+  h->agent = agent; h->agrad = agent_grad; h->asq = agent_sq; h->critic = critic; h->tcritic = target_critic;
+  h->cgrad = critic_grad; h->csq = critic_sq; h->stats = stats;
+  // the agent handle: online = target = the agent params (the actor has no target net); stats land at stats + 8
+  return mq_bind(h->ah, agent, agent, agent_grad, agent_sq, stats + 8, nullptr);
+}
+
+int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* stream) {
+  if (!h || !h->agent) return set_err(MQ_ERR_STATE, "mc_train_step before mc_bind");
+  mq_handle* ah = h->ah;
+  int rc = check_batch(ah, batch);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const mc_config& c = h->cfg;
+  const int n = c.n_agents, A = c.n_actions;
+  const int Tp = batch->t_len, T = Tp - 1, R = batch->batch_size * n;
+  const Rep rp = make_rep(batch);
+
+  CDims cd;
+  cd.n = n; cd.A = A; cd.O = c.obs_dim; cd.S = c.state_dim; cd.Kc = h->Kc; cd.Kp = h->Kp; cd.R = R;
+  cd.B = batch->batch_size; cd.Tp = Tp; cd.T = T; cd.t_stride = batch->t_stride;
+  cd.lg = (float)((double)c.td_lambda * (double)c.gamma);
+  cd.og = (float)((1.0 - (double)c.td_lambda) * (double)c.gamma);
+  cd.dR = make_fastdiv((uint32_t)R);
+  cd.dN = make_fastdiv((uint32_t)n);
+
+  MQ_HIP(hipMemsetAsync(h->crec, 0, (size_t)T * 8 * sizeof(float), s));
+  MQ_HIP(hipMemsetAsync(h->cstate, 0, 4 * sizeof(int), s));
+  hipLaunchKernelGGL(coma_mask_kernel, dim3((T + 255) / 256), dim3(256), 0, s, cd, rp, h->msum);
+  MQ_HIP(hipGetLastError());
+  hipLaunchKernelGGL(coma_xin_kernel, dim3(Tp * R), dim3(256), 0, s, cd, rp, h->X);
+  MQ_HIP(hipGetLastError());
+  // target critic over every stored step (coma_learner.py:102), then TD(lambda) (rl_utils.py:4-14)
+  {
+    const int64_t M = (int64_t)Tp * R;
+    const float* tc = h->tcritic;
+    CLinProb l1{h->X, h->Kp, tc + h->coff[MC_P_FC1_W], tc + h->coff[MC_P_FC1_B], h->H1t, M, CH, h->Kc, 1};
+    MQ_HIP(launch_gemm(l1, (int)M, CH, 1, s));
+    CLinProb l2{h->H1t, CH, tc + h->coff[MC_P_FC2_W], tc + h->coff[MC_P_FC2_B], h->H2t, M, CH, CH, 1};
+    MQ_HIP(launch_gemm(l2, (int)M, CH, 1, s));
+    CLinProb l3{h->H2t, CH, tc + h->coff[MC_P_FC3_W], tc + h->coff[MC_P_FC3_B], h->Qt, M, A, CH, 0};
+    MQ_HIP(launch_gemm(l3, (int)M, A, 1, s));
+  }
+  hipLaunchKernelGGL(coma_td_kernel, dim3((R + 63) / 64), dim3(64), 0, s, cd, rp, h->Qt, h->tgt);
+  MQ_HIP(hipGetLastError());
+
+  // the critic's T sequential steps (coma_learner.py:118-139)
+  CritArgs ca;
+  ca.d = cd; ca.rp = rp;
+  ca.P[0] = h->critic; ca.P[1] = h->Pshadow; ca.SQ[0] = h->csq; ca.SQ[1] = h->SQshadow; ca.G = h->cgrad;
+  ca.o_w1 = h->coff[MC_P_FC1_W]; ca.o_b1 = h->coff[MC_P_FC1_B]; ca.o_w2 = h->coff[MC_P_FC2_W];
+  ca.o_b2 = h->coff[MC_P_FC2_B]; ca.o_w3 = h->coff[MC_P_FC3_W]; ca.o_b3 = h->coff[MC_P_FC3_B]; ca.Pc = h->Pc;
+  ca.X = h->X; ca.tgt = h->tgt; ca.msum = h->msum; ca.H1c = h->H1c; ca.H2c = h->H2c; ca.dH1c = h->dH1c;
+  ca.dH2c = h->dH2c; ca.dqc = h->dqc; ca.actc = h->actc; ca.qvals = h->qvals; ca.cpart = h->cpart;
+  ca.cnorm = h->cnorm; ca.crec = h->crec; ca.cstate = h->cstate;
+  ca.nhead = (R + 15) / 16;
+  ca.nwgrad = wgrad_blocks(cd);
+  ca.hp = OptHP{c.critic_lr, c.optim_alpha, c.optim_eps, c.grad_norm_clip, 1};
+  const int A16 = (A + 15) / 16 * 16;
+  const size_t lds_l1 = ((size_t)2 * 16 * (h->Kp + 1) + 4 * 16 * 16) * sizeof(float);
+  const size_t lds_head = ((size_t)(CH + A16 + 48) * (CH + 1) + 16 * (A16 + 1) + CH + A16) * sizeof(float);
+  if (lds_l1 > 160 * 1024 || lds_head > 160 * 1024)
+    return set_err(MQ_ERR_ARG, "critic input width or n_actions too large for the LDS-staged critic step");
+  MQ_HIP(hipMemsetAsync(h->qvals, 0, (size_t)T * R * A * sizeof(float), s));   // skipped steps keep q_vals = 0
+  for (int t = T - 1; t >= 0; --t) {
+    hipLaunchKernelGGL(coma_l1_kernel, dim3(ca.nhead, CH / 16), dim3(256), lds_l1, s, ca, t);
+    hipLaunchKernelGGL(coma_head_kernel, dim3(ca.nhead), dim3(256), lds_head, s, ca, t);
+    hipLaunchKernelGGL(coma_wgrad_kernel, dim3(ca.nwgrad), dim3(256), 0, s, ca, t);
+  }
+  MQ_HIP(hipGetLastError());
+  hipLaunchKernelGGL(coma_capply_kernel, dim3((int)std::min<int64_t>((h->Pc + 255) / 256, 512)), dim3(256), 0, s,
+                     ca);
+  MQ_HIP(hipGetLastError());
+
+  // ---- actor: the agent unroll over t < T (coma_learner.py:52-57), online net only
+  mq_replay av = *batch;
+  av.t_len = T;
+  Dims d = make_dims(ah, &av);
+  const Lay L = make_lay(ah);
+  Work w = ah->w;
+  w.dHo = h->dHo;
+  const int64_t RT = (int64_t)T * R;
+  const float* Pa = h->agent;
+  const int rw_fwd = pick_rw(d.R, 512);
+  if (rw_fwd == 1 && fused_fwd_ok(d.I, d.O, d.A, d.n, RT)) {
+    hipLaunchKernelGGL(gru_fwd_fused_kernel<0>, dim3(d.R, 1), dim3(512), 0, s, d, rp, Pa, Pa, L, w);
+    MQ_HIP(hipGetLastError());
+  } else {
+    Fc1Prob p1{d, rp, Pa, Pa, ah->off[MQ_P_FC1_W], ah->off[MQ_P_FC1_B], w.X1, w.XIN, RT};
+    MQ_HIP(launch_gemm(p1, (int)RT, 2 * mq::H, 1, s));
+    GiProb p2{w.X1, Pa, Pa, ah->off[MQ_P_RNN_W_IH], ah->off[MQ_P_RNN_B_IH], w.GI, RT};
+    MQ_HIP(launch_gemm(p2, (int)RT, mq::G3, 1, s));
+    const dim3 grid((d.R + rw_fwd - 1) / rw_fwd, 1);
+    if (rw_fwd == 1) hipLaunchKernelGGL((gru_fwd_kernel<1, 0>), grid, dim3(256), 0, s, d, Pa, Pa, L, w);
+    else if (rw_fwd == 2) hipLaunchKernelGGL((gru_fwd_kernel<2, 0>), grid, dim3(256), 0, s, d, Pa, Pa, L, w);
+    else if (rw_fwd == 4) hipLaunchKernelGGL((gru_fwd_kernel<4, 0>), grid, dim3(256), 0, s, d, Pa, Pa, L, w);
+    else hipLaunchKernelGGL((gru_fwd_kernel<8, 0>), grid, dim3(256), 0, s, d, Pa, Pa, L, w);
+    MQ_HIP(hipGetLastError());
+    Fc2Prob p3{w.Hs, Pa, Pa, ah->off[MQ_P_FC2_W], ah->off[MQ_P_FC2_B], w.Q, RT, d.A};
+    MQ_HIP(launch_gemm(p3, (int)RT, d.A, 1, s));
+  }
+  // policy, baseline, advantage, loss sums and dLogits (coma_learner.py:59-77, basic_controller.py:53-73)
+  const int npol = (int)((RT + 3) / 4);
+  const float eps = epsilon, omeps = (float)(1.0 - (double)epsilon);
+  hipLaunchKernelGGL(coma_policy_kernel, dim3(npol), dim3(256), 0, s, d, rp, (const float*)w.Q,
+                     (const float*)h->qvals, eps, omeps, (int)(c.mask_before_softmax != 0), h->Ap, h->dL, h->pi,
+                     h->ppart);
+  MQ_HIP(hipGetLastError());
+  // BPTT with the dense output gradient
+  {
+    DhoProb p{h->dL, h->Ap, A, Pa + ah->off[MQ_P_FC2_W], h->dHo, RT};
+    MQ_HIP(launch_gemm(p, (int)RT, mq::H, 1, s));
+  }
+  const int rw_bwd = std::min(2, pick_rw(d.R, 256));
+  int nblk_bwd = (d.R + rw_bwd - 1) / rw_bwd;
+  const size_t dyn = ((size_t)2 * d.A * mq::H + d.A) * sizeof(float);
+  if (rw_bwd == 1)
+    hipLaunchKernelGGL((gru_bwd_kernel<1, 0, true>), dim3(nblk_bwd), dim3(512), dyn, s, d, rp, Pa, L, w, ah->len_rnn);
+  else
+    hipLaunchKernelGGL((gru_bwd_kernel<2, 0, true>), dim3(nblk_bwd), dim3(512), dyn, s, d, rp, Pa, L, w, ah->len_rnn);
+  MQ_HIP(hipGetLastError());
+  {
+    Dx1Prob p{w.dGI, Pa + ah->off[MQ_P_RNN_W_IH], w.X1, w.dP1, RT};
+    MQ_HIP(launch_gemm(p, (int)RT, mq::H, 1, s));
+  }
+  int ns1;
+  {
+    const int tiles = (d.I + Dw1Prob::BN - 1) / Dw1Prob::BN;
+    int ns = (int)std::min<int64_t>(kNsplitMax, std::max<int64_t>(1, RT / 256));
+    ns = std::max(1, std::min(ns, (512 + tiles - 1) / tiles));
+    int64_t chunk = ((RT + ns - 1) / ns + GBK - 1) / GBK * GBK;
+    ns = (int)((RT + chunk - 1) / chunk);
+    ns1 = ns;
+    Dw1Prob p{d.I, w.dP1, w.XIN, w.slab_fc1, RT, ns};
+    MQ_HIP(launch_gemm(p, mq::H, d.I, ns, s));
+  }
+  int ns2;
+  {
+    int ns = (int)std::min<int64_t>(kNsplitMax, std::max<int64_t>(1, RT / 256));
+    int64_t chunk = ((RT + ns - 1) / ns + GBK - 1) / GBK * GBK;
+    ns = (int)((RT + chunk - 1) / chunk);
+    ns2 = ns;
+    Dw2Prob p{h->dL, h->Ap, A, w.Hs, h->slab_fc2, RT, ns};
+    MQ_HIP(launch_gemm(p, A, mq::H, ns, s));
+  }
+  int nnorm;
+  {
+    RedBuilder rb(h->red_tmp);
+    rb.add(w.slab_fc1, ns1, (int64_t)mq::H * d.I + mq::H, h->agrad + ah->off[MQ_P_FC1_W], true);
+    // W_ih .. b_hh: the prefix of each BPTT slab (its fc2 part is unused in the dense-dy mode)
+    rb.add(w.slab_rnn, nblk_bwd, ah->off[MQ_P_FC2_W] - ah->off[MQ_P_RNN_W_IH], h->agrad + ah->off[MQ_P_RNN_W_IH],
+           true, ah->len_rnn);
+    rb.add(h->slab_fc2, ns2, (int64_t)A * mq::H + A, h->agrad + ah->off[MQ_P_FC2_W], true);
+    rb.add(h->ppart, npol, MQ_NSUMS, h->agrad + h->Pa, false);
+    hipLaunchKernelGGL(red_pass1_kernel, dim3(rb.b1), dim3(256), 0, s, rb.pl);
+    MQ_HIP(hipGetLastError());
+    if (rb.b2 > 4096) return set_err(MQ_ERR_ARG, "agent too large for the norm partial buffer");
+    hipLaunchKernelGGL(red_pass2_kernel, dim3(rb.b2), dim3(256), 0, s, rb.pl, h->norm_part);
+    MQ_HIP(hipGetLastError());
+    nnorm = rb.b2;
+  }
+  {
+    OptHP hp{c.lr, c.optim_alpha, c.optim_eps, c.grad_norm_clip, 1};
+    const int blocks = (int)std::min<int64_t>((h->Pa + 255) / 256, 1024);
+    hipLaunchKernelGGL(apply_kernel, dim3(blocks), dim3(256), 0, s, h->agent, h->agrad, h->asq, h->Pa,
+                       (const float*)h->norm_part, nnorm, hp, h->stats + 8);
+    MQ_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(coma_stats_kernel, dim3(1), dim3(64), 0, s, (const float*)h->crec, T,
+                     (const int*)h->cstate, h->stats);
+  MQ_HIP(hipGetLastError());
+  h->last_T = T;
+  h->last_R = R;
+  return MQ_OK;
+}
+
+int mc_update_targets(mc_handle* h, void* stream) {
+  if (!h || !h->critic) return set_err(MQ_ERR_STATE, "mc_update_targets before mc_bind");
+  MQ_HIP(hipMemcpyAsync(h->tcritic, h->critic, h->Pc * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return MQ_OK;
+}
+
+int mc_policy(float* logits, const int32_t* avail, int32_t rows, int32_t n_actions, float epsilon,
+              int32_t mask_before_softmax, int32_t test_mode, void* stream) {
+  if (!logits || !avail || rows < 0 || n_actions < 1 || n_actions > 64) return set_err(MQ_ERR_ARG, "bad mc_policy args");
+  if (rows == 0) return MQ_OK;
+  hipLaunchKernelGGL(mc_policy_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, logits, avail,
+                     (int)rows, (int)n_actions, epsilon, (int)mask_before_softmax, (int)test_mode);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+int mc_copy_intermediate(mc_handle* h, int which, float* dst, int64_t* count, void* stream) {
+  if (!h || h->last_T <= 0) return set_err(MQ_ERR_STATE, "no COMA train step has run");
+  const int64_t TR = (int64_t)h->last_T * h->last_R;
+  const float* src;
+  int64_t cnt;
+  switch (which) {
+    case 0: src = h->qvals; cnt = TR * h->cfg.n_actions; break;
+    case 1: src = h->tgt; cnt = TR; break;
+    case 2: src = h->pi; cnt = TR * h->cfg.n_actions; break;
+    default: return set_err(MQ_ERR_ARG, "unknown COMA intermediate id");
+  }
+  if (count) *count = cnt;
+  if (dst) MQ_HIP(hipMemcpyAsync(dst, src, cnt * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return MQ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,760 @@
+// COMA learner kernels: the centralised critic's T sequential RMSprop steps and the
+// counterfactual policy-gradient step of COMALearner.train (coma_learner.py:32-148), gfx950, fp32 throughout.
+//
+// Critic (coma.py:22-58, fc 868 -> 128 -> 128 -> A at MMM2). Each train() takes one optimiser step per t in
+// reversed order, every step on B*n rows only, so the critic is a chain of T tiny dependent steps. One step is three
+// launches, split where the data dependence forces a grid-wide exchange:
+//   l1     H1 = relu(X_t W1^T + b1)                 grid (row tiles of 16) x (8 unit tiles of 16)
+//   head   H2, Q, TD error, loss sums, dQ, dH2, dH1 grid (row tiles of 16): rows are independent up to dH1
+//   wgrad  dW1 = dH1^T X_t, dW2 = dH2^T H1, dW3, biases, per-workgroup sums of squares (each gradient element has
+//          exactly one writer: no slabs, no atomics)
+// The RMSprop update of step t+1 (clip coefficient from wgrad's sums of squares) is applied by the NEXT step's l1
+// (its W1 / b1 tile) and head (W2, b2, W3, b3) right where they stage the weights, so applying costs no launch;
+// the last step's update is one more launch after the loop. Every workgroup that stages a tile applies the update
+// to it in LDS; one designated workgroup writes params / square_avg / clipped grads back.
+// Steps whose mask is empty are skipped on the device (coma_learner.py:121-122) and leave the pending update for the
+// next live step.
+//
+// MFMA: v_mfma_f32_16x16x4_f32 (exact fp32 FMA chain). Lane l, g = l >> 4, c = l & 15: A[i = c][kk = g],
+// B[kk = g][j = c], D[i = 4g + reg][j = c].
+#pragma once
+#include "learner_gemms.hpp"
+#include "optim_kernels.hpp"
+
+namespace mq {
+
+constexpr int CH = 128;   // critic hidden width (coma.py:17-19)
+
+MQ_DEV f32x4 mfma_f32_16x4(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+MQ_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+struct CDims {
+  int n, A, O, S, Kc, Kp, R, B, Tp, T, t_stride;
+  float lg, og;      // f32(td_lambda * gamma), f32((1 - td_lambda) * gamma): rounded on the host in double, as the
+                     // reference's Python-float scalar products are
+  FastDiv dR, dN;
+};
+
+// reference mask (coma_learner.py:39-41): filled[t] * (1 - terminated[t-1])
+MQ_DEV float coma_mask(const Rep& rp, int64_t slot, int t) {
+  float m = (float)rp.filled[slot];
+  if (t > 0) m *= 1.0f - (float)rp.term[slot - 1];
+  return m;
+}
+
+// ------------------------------------------------------------------------------------------- critic inputs
+// X[t][r][k] for every stored step of the batch (COMACritic._build_inputs, coma.py:30-58):
+// state | obs | actions_onehot[t] of every agent with the row's own block zeroed | actions_onehot[t-1] (0 at t = 0)
+// | onehot(agent) | zero padding to Kp. actions_onehot is the reference's OneHot transform of the stored action,
+// zero on unfilled slots (the runner never writes them).
+__global__ __launch_bounds__(256) void coma_xin_kernel(CDims d, Rep rp, float* __restrict__ X) {
+  const int tr = blockIdx.x;
+  const int t = (int)fdiv((uint32_t)tr, d.dR), r = tr - t * d.R;
+  const int b = (int)fdiv((uint32_t)r, d.dN), ag = r - b * d.n;
+  const int64_t slot = rp.ep(b) * d.t_stride + t;
+  const float* st = rp.state + slot * d.S;
+  const float* ob = rp.obs + (slot * d.n + ag) * d.O;
+  const int nA = d.n * d.A, k1 = d.S + d.O, k2 = k1 + nA, k3 = k2 + nA;
+  const bool fill_t = rp.filled[slot] != 0, fill_p = t > 0 && rp.filled[slot - 1] != 0;
+  float* out = X + (int64_t)tr * d.Kp;
+  for (int k = threadIdx.x; k < d.Kp; k += 256) {
+    float v = 0.0f;
+    if (k < d.S) {
+      v = st[k];
+    } else if (k < k1) {
+      v = ob[k - d.S];
+    } else if (k < k2) {
+      const int j = (k - k1) / d.A, a = (k - k1) - j * d.A;
+      v = (j != ag && fill_t && rp.actions[slot * d.n + j] == a) ? 1.0f : 0.0f;
+    } else if (k < k3) {
+      const int j = (k - k2) / d.A, a = (k - k2) - j * d.A;
+      v = (fill_p && rp.actions[(slot - 1) * d.n + j] == a) ? 1.0f : 0.0f;
+    } else if (k < d.Kc) {
+      v = (k - k3) == ag ? 1.0f : 0.0f;
+    }
+    out[k] = v;
+  }
+}
+
+// Sum of the critic mask of step t over (episode, agent) (mask_t.sum(), coma_learner.py:120-122), t < T.
+__global__ __launch_bounds__(256) void coma_mask_kernel(CDims d, Rep rp, float* __restrict__ msum) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= d.T) return;
+  float s = 0.0f;
+  for (int b = 0; b < d.B; ++b) s += coma_mask(rp, rp.ep(b) * d.t_stride + t, t);
+  msum[t] = s * (float)d.n;
+}
+
+// Dense linear layer for the target critic's all-steps forward: out[m][j] = act(X[m][:K] . W[j][:K] + bias[j]).
+struct CLinProb {
+  static constexpr int BN = 128;
+  const float* X;   // [M][ldx]
+  int ldx;
+  const float* W;   // [N][K] row-major (the reference layout)
+  const float* bias;
+  float* out;       // [M][N]
+  int64_t M;
+  int N, K, relu;
+  using APat = KPat;
+  using BPat = KPat;
+  static constexpr bool kRowSum = false;
+  struct Ctx {
+    const float* arow;
+    const float* brow[2];
+  };
+  MQ_DEV Ctx make_ctx(int m0, int n0, int, int tid) const {
+    Ctx c;
+    const int64_t m = m0 + KPat::row(tid);
+    c.arow = m < M ? X + m * ldx : nullptr;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int nn = n0 + 64 * p + KPat::row(tid);
+      c.brow[p] = nn < N ? W + (int64_t)nn * K : nullptr;
+    }
+    return c;
+  }
+  MQ_DEV void krange(int, int& kb, int& ke) const { kb = 0; ke = K; }
+  MQ_DEV void load_a(const Ctx& c, int k0, int ke, float (&r)[4]) const {
+    const int k = k0 + KPat::kq(threadIdx.x);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = (c.arow && k + i < ke) ? c.arow[k + i] : 0.0f;
+  }
+  MQ_DEV void load_b(const Ctx& c, int pass, int k0, int ke, float (&r)[4]) const {
+    const int k = k0 + KPat::kq(threadIdx.x);
+    const float* p = c.brow[pass];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = (p && k + i < ke) ? p[k + i] : 0.0f;
+  }
+  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int, int lane) const {
+    const int j = ncol0 + (lane & 31);
+    if (j >= N) return;
+    const float bj = bias[j];
+    for_tile(acc, mrow0, ncol0, lane, [&](int m, int jj, float v) {
+      if (m < M) {
+        const float y = v + bj;
+        out[(int64_t)m * N + jj] = relu ? fmaxf(y, 0.0f) : y;
+      }
+    });
+  }
+  MQ_DEV void rowsum_out(int, int, float) const {}
+};
+
+// build_td_lambda_targets (rl_utils.py:4-14) for one (episode, agent) column per thread: the backward recursion
+// ret_t = lambda gamma ret_{t+1} + mask_t (r_t + (1 - lambda) gamma Q'_{t+1}(a_{t+1}) (1 - term_t)),
+// ret_{T} = Q'_T(a_T) (1 - sum_t term_t). Writes targets [T][R].
+__global__ __launch_bounds__(64) void coma_td_kernel(CDims d, Rep rp, const float* __restrict__ Qt,
+                                                     float* __restrict__ tgt) {
+  const int r = blockIdx.x * 64 + threadIdx.x;
+  if (r >= d.R) return;
+  const int b = (int)fdiv((uint32_t)r, d.dN), ag = r - b * d.n;
+  const int64_t e0 = rp.ep(b) * d.t_stride;
+  auto taken = [&](int t) { return Qt[((int64_t)t * d.R + r) * d.A + (int)rp.actions[(e0 + t) * d.n + ag]]; };
+  float tsum = 0.0f;
+  for (int t = 0; t < d.T; ++t) tsum += (float)rp.term[e0 + t];
+  float ret = taken(d.Tp - 1) * (1.0f - tsum);
+  for (int t = d.Tp - 2; t >= 0; --t) {
+    const int64_t slot = e0 + t;
+    const float m = coma_mask(rp, slot, t);
+    // torch's evaluation order, no FMA contraction
+    const float inner = __fadd_rn(rp.reward[slot], __fmul_rn(__fmul_rn(d.og, taken(t + 1)), 1.0f - (float)rp.term[slot]));
+    ret = __fadd_rn(__fmul_rn(d.lg, ret), __fmul_rn(m, inner));
+    tgt[(int64_t)t * d.R + r] = ret;
+  }
+}
+
+// ------------------------------------------------------------------------------------------ critic steps
+struct CritArgs {
+  CDims d;
+  Rep rp;
+  float* P[2];       // critic params (reference layout): [0] the caller's buffer, [1] a shadow. Live step L reads
+  float* SQ[2];      // version L-1 from [(L-1) & 1] and writes version L to [L & 1] (no block ever reads what
+                     // another block of the same launch writes); the last update lands in [0]
+  float* G;          // raw critic grads of the pending (last live) step [Pc] + tail: [0] = its mask sum
+  int64_t o_w1, o_b1, o_w2, o_b2, o_w3, o_b3, Pc;
+  const float* X;    // [Tp][R][Kp]
+  const float* tgt;  // [T][R]
+  const float* msum; // [T]
+  float* H1c;        // [R][CH] this step's activations / gradients
+  float* H2c;
+  float* dH1c;
+  float* dH2c;
+  float* dqc;        // [R]
+  int* actc;         // [R]
+  float* qvals;      // [T][R][A]
+  float* cpart;      // [head blocks][8]
+  float* cnorm;      // [wgrad blocks]
+  int nhead, nwgrad;
+  float* crec;       // [T][8]: sum (td m)^2, sum m, sum |td m|, sum q m, sum y m, grad norm, live
+  int* cstate;       // [0] live steps so far, [1] t of the last live step
+  OptHP hp;
+};
+
+// Clip coefficient of the pending critic update (clip_grad_norm_ over the critic, coma_learner.py:133): every block
+// re-derives it from the same partials in the same order, so all blocks agree bitwise.
+MQ_DEV void crit_coef(const CritArgs& a, float* sh) {
+  if (threadIdx.x < 64) {
+    float s = 0.0f;
+    for (int i = threadIdx.x; i < a.nwgrad; i += 64) s += a.cnorm[i];
+    s = wave_sum(s);
+    if (threadIdx.x == 0) {
+      const float inv = 1.0f / a.G[a.Pc];
+      const float norm = sqrtf(s) * inv;
+      sh[0] = inv;
+      sh[1] = fminf(a.hp.clip / (norm + 1e-6f), 1.0f);
+      sh[2] = norm;
+    }
+  }
+}
+
+// RMSprop on one element of the pending update (torch: v = a v + (1-a) g^2; p += -lr g / (sqrt(v) + eps)), from
+// buffer src into buffer dst (write = the designated block).
+MQ_DEV float crit_rms(const CritArgs& a, int64_t i, float inv, float coef, int src, int dst, bool write) {
+  const float g = (a.G[i] * inv) * coef;
+  const float v = a.SQ[src][i] * a.hp.alpha + (1.0f - a.hp.alpha) * (g * g);
+  const float p = a.P[src][i] + (-a.hp.lr) * (g / (sqrtf(v) + a.hp.eps));
+  if (write) { a.SQ[dst][i] = v; a.P[dst][i] = p; }
+  return p;
+}
+
+// Stage elements [0, N) of a parameter region into LDS (dst_lds(e) <- parameter o + idx(e)), applying the pending
+// update on the way. All loads of a batch of kStageB elements per thread are issued before any use: the loop is
+// latency-bound (G / square_avg / params come from L2 or HBM), not issue-bound.
+constexpr int kStageB = 16;
+template <class Idx, class Put>
+MQ_DEV void crit_stage(const CritArgs& a, int N, bool pend, float inv, float coef, int src, int dst, bool owner,
+                       Idx idx, Put put) {
+  for (int e0 = threadIdx.x; e0 < N; e0 += 256 * kStageB) {
+    float gv[kStageB], sv[kStageB], pv[kStageB];
+#pragma unroll
+    for (int u = 0; u < kStageB; ++u) {
+      const int e = e0 + 256 * u;
+      const int64_t i = idx(e < N ? e : N - 1);
+      pv[u] = a.P[src][i];
+      if (pend) { gv[u] = a.G[i]; sv[u] = a.SQ[src][i]; }
+    }
+#pragma unroll
+    for (int u = 0; u < kStageB; ++u) {
+      const int e = e0 + 256 * u;
+      if (e >= N) break;
+      float p = pv[u];
+      if (pend) {
+        const float g = (gv[u] * inv) * coef;
+        const float v = sv[u] * a.hp.alpha + (1.0f - a.hp.alpha) * (g * g);
+        p = p + (-a.hp.lr) * (g / (sqrtf(v) + a.hp.eps));
+        if (owner) {
+          const int64_t i = idx(e);
+          a.SQ[dst][i] = v;
+          a.P[dst][i] = p;
+        }
+      }
+      put(e, p);
+    }
+  }
+}
+
+// l1: H1 = relu(X_t W1^T + b1) for a 16-row x 16-unit tile; K split over the 4 waves.
+__global__ __launch_bounds__(256) void coma_l1_kernel(CritArgs a, int t) {
+  if (!(a.msum[t] > 0.0f)) return;
+  extern __shared__ float sm[];
+  const int Kp = a.d.Kp, KP = Kp + 1, Kc = a.d.Kc, R = a.d.R;
+  float* Ws = sm;               // [16][KP]
+  float* Xs = Ws + 16 * KP;     // [16][KP]
+  float* red = Xs + 16 * KP;    // [4][16][16]
+  __shared__ float sh[4];
+  __shared__ float bs[16];
+  const int tid = threadIdx.x, u0 = blockIdx.y * 16, r0 = blockIdx.x * 16;
+  const int L = a.cstate[0];
+  const bool pend = L > 0, owner = blockIdx.x == 0;
+  const int src = pend ? (L - 1) & 1 : 0, dst = L & 1;
+  if (pend) crit_coef(a, sh);
+  __syncthreads();
+  const float inv = pend ? sh[0] : 0.0f, coef = pend ? sh[1] : 0.0f;
+  if (pend && owner && blockIdx.y == 0 && tid == 0) a.crec[a.cstate[1] * 8 + 5] = sh[2];
+  // W1 rows u0 .. u0+15 (contiguous in the reference layout: 16 * Kc elements), zero-padded to Kp in LDS
+  for (int e = tid; e < 16 * (Kp - Kc); e += 256) Ws[(e / (Kp - Kc)) * KP + Kc + e % (Kp - Kc)] = 0.0f;
+  crit_stage(a, 16 * Kc, pend, inv, coef, src, dst, owner,
+             [&](int e) { return a.o_w1 + (int64_t)u0 * Kc + e; },
+             [&](int e, float v) { const int u = e / Kc; Ws[u * KP + (e - u * Kc)] = v; });
+  crit_stage(a, 16, pend, inv, coef, src, dst, owner, [&](int e) { return a.o_b1 + u0 + e; },
+             [&](int e, float v) { bs[e] = v; });
+  if (pend) {   // fc2 / fc3 (contiguous [o_w2, Pc)): each l1 block updates one slice, head reads the result
+    const int nb = gridDim.x * gridDim.y, lb = blockIdx.y * gridDim.x + blockIdx.x;
+    const int64_t NT = a.Pc - a.o_w2, chunk = (NT + nb - 1) / nb, beg = lb * chunk;
+    const int cnt = (int)max<int64_t>(0, min<int64_t>(chunk, NT - beg));
+    crit_stage(a, cnt, true, inv, coef, src, dst, true, [&](int e) { return a.o_w2 + beg + e; },
+               [&](int, float) {});
+  }
+  {   // X_t rows r0 .. r0+15: b128 loads, all in flight before the LDS stores
+    const int nv = Kp / 4;
+    constexpr int XB = 8;
+    for (int e0 = tid; e0 < 16 * nv; e0 += 256 * XB) {
+      f32x4 xv[XB];
+#pragma unroll
+      for (int u = 0; u < XB; ++u) {
+        const int e = min(e0 + 256 * u, 16 * nv - 1), rr = e / nv, kv = e - rr * nv;
+        xv[u] = r0 + rr < R ? *(const f32x4*)&a.X[((int64_t)t * R + r0 + rr) * Kp + 4 * kv] : f32x4{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int u = 0; u < XB; ++u) {
+        const int e = e0 + 256 * u;
+        if (e >= 16 * nv) break;
+        const int rr = e / nv, kv = e - rr * nv;
+        float* d = &Xs[rr * KP + 4 * kv];
+        d[0] = xv[u][0]; d[1] = xv[u][1]; d[2] = xv[u][2]; d[3] = xv[u][3];
+      }
+    }
+  }
+  __syncthreads();
+  const int w = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
+  const int Kq = (Kp + 15) / 16 * 4;
+  const int kb = w * Kq, ke = min(Kp, kb + Kq);
+  f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+  int k = kb;
+  for (; k + 8 <= ke; k += 8) {
+    acc0 = mfma_f32_16x4(Xs[c * KP + k + g], Ws[c * KP + k + g], acc0);
+    acc1 = mfma_f32_16x4(Xs[c * KP + k + 4 + g], Ws[c * KP + k + 4 + g], acc1);
+  }
+  if (k < ke) acc0 = mfma_f32_16x4(Xs[c * KP + k + g], Ws[c * KP + k + g], acc0);
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) red[(w * 16 + 4 * g + reg) * 16 + c] = acc0[reg] + acc1[reg];
+  __syncthreads();
+  {
+    const int i = tid >> 4, j = tid & 15;
+    const float v = ((red[(0 * 16 + i) * 16 + j] + red[(1 * 16 + i) * 16 + j]) +
+                     (red[(2 * 16 + i) * 16 + j] + red[(3 * 16 + i) * 16 + j])) + bs[j];
+    if (r0 + i < R) a.H1c[(int64_t)(r0 + i) * CH + u0 + j] = fmaxf(v, 0.0f);
+  }
+}
+
+// head: for a 16-row tile, H2 = relu(H1 W2^T + b2), Q = H2 W3^T + b3, the TD error against the TD(lambda) target,
+// the loss sums, dQ (unnormalised: d sum (td m)^2 / dq_taken = 2 td m m), dH2 = dQ W3 o [H2 > 0], dH1 = dH2 W2 o
+// [H1 > 0]. Stages (and applies the pending update to) W2 / b2 / W3 / b3; block 0 writes them back.
+__global__ __launch_bounds__(256) void coma_head_kernel(CritArgs a, int t) {
+  if (!(a.msum[t] > 0.0f)) return;
+  extern __shared__ float sm[];
+  constexpr int CP = CH + 1;
+  const int A = a.d.A, A16 = (A + 15) / 16 * 16, R = a.d.R, n = a.d.n;
+  float* W2s = sm;                 // [CH][CP]
+  float* W3s = W2s + CH * CP;      // [A16][CP]
+  float* H1s = W3s + A16 * CP;     // [16][CP]
+  float* H2s = H1s + 16 * CP;      // [16][CP]
+  float* dHs = H2s + 16 * CP;      // [16][CP]
+  float* Qs = dHs + 16 * CP;       // [16][A16 + 1]
+  float* b2s = Qs + 16 * (A16 + 1);   // [CH]
+  float* b3s = b2s + CH;              // [A16]
+  __shared__ float dqs[16];
+  __shared__ int acts[16];
+  __shared__ float part[16][5];
+  const int tid = threadIdx.x, r0 = blockIdx.x * 16;
+  // fc2 / fc3 at this step's version (l1 applied the pending update into P[L & 1])
+  const float* Pv = a.P[a.cstate[0] & 1];
+  {
+    constexpr int NB = 16;
+    const int N2 = CH * CH / 4, N3 = A * CH / 4;   // b128 units (CH = 128: rows never straddle a unit)
+    for (int e0 = tid; e0 < N2 + N3; e0 += 256 * NB) {
+      f32x4 v[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int e = min(e0 + 256 * u, N2 + N3 - 1);
+        v[u] = e < N2 ? *(const f32x4*)&Pv[a.o_w2 + 4 * e] : *(const f32x4*)&Pv[a.o_w3 + 4 * (e - N2)];
+      }
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int e = e0 + 256 * u;
+        if (e >= N2 + N3) break;
+        float* d = e < N2 ? &W2s[((4 * e) >> 7) * CP + ((4 * e) & 127)]
+                          : &W3s[((4 * (e - N2)) >> 7) * CP + ((4 * (e - N2)) & 127)];
+        d[0] = v[u][0]; d[1] = v[u][1]; d[2] = v[u][2]; d[3] = v[u][3];
+      }
+    }
+  }
+  for (int e = A * CH + tid; e < A16 * CH; e += 256) W3s[(e >> 7) * CP + (e & 127)] = 0.0f;
+  if (tid < CH) b2s[tid] = Pv[a.o_b2 + tid];
+  if (tid < A) b3s[tid] = Pv[a.o_b3 + tid];
+  if (tid >= A && tid < A16) b3s[tid] = 0.0f;
+  {
+    f32x4 hv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + 256 * u, i = e >> 5, kv = e & 31;
+      hv[u] = r0 + i < R ? *(const f32x4*)&a.H1c[(int64_t)(r0 + i) * CH + 4 * kv] : f32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + 256 * u, i = e >> 5, kv = e & 31;
+      float* d = &H1s[i * CP + 4 * kv];
+      d[0] = hv[u][0]; d[1] = hv[u][1]; d[2] = hv[u][2]; d[3] = hv[u][3];
+    }
+  }
+  __syncthreads();
+  const int w = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
+  // H2 = relu(H1 W2^T + b2): wave w owns unit tiles w and w + 4
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int jt = w + 4 * jj;
+    f32x4 acc = {0, 0, 0, 0};
+    for (int k = 0; k < CH; k += 4) acc = mfma_f32_16x4(H1s[c * CP + k + g], W2s[(16 * jt + c) * CP + k + g], acc);
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg)
+      H2s[(4 * g + reg) * CP + 16 * jt + c] = fmaxf(acc[reg] + b2s[16 * jt + c], 0.0f);
+  }
+  __syncthreads();
+  // Q = H2 W3^T + b3
+  for (int qt = w; qt < A16 / 16; qt += 4) {
+    f32x4 acc = {0, 0, 0, 0};
+    for (int k = 0; k < CH; k += 4) acc = mfma_f32_16x4(H2s[c * CP + k + g], W3s[(16 * qt + c) * CP + k + g], acc);
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) Qs[(4 * g + reg) * (A16 + 1) + 16 * qt + c] = acc[reg] + b3s[16 * qt + c];
+  }
+  __syncthreads();
+  // TD error, loss sums, dQ at the taken action (coma_learner.py:124-131)
+  if (tid < 16) {
+    const int rr = r0 + tid;
+    float m = 0.0f, q = 0.0f, y = 0.0f, dq = 0.0f;
+    int at = 0;
+    if (rr < R) {
+      const int b = (int)fdiv((uint32_t)rr, a.d.dN), ag = rr - b * n;
+      const int64_t slot = a.rp.ep(b) * a.d.t_stride + t;
+      at = (int)a.rp.actions[slot * n + ag];
+      m = coma_mask(a.rp, slot, t);
+      q = Qs[tid * (A16 + 1) + at];
+      y = a.tgt[(int64_t)t * R + rr];
+      const float mtd = (q - y) * m;
+      dq = (2.0f * mtd) * m;
+      part[tid][0] = mtd * mtd; part[tid][1] = m; part[tid][2] = fabsf(mtd); part[tid][3] = q * m;
+      part[tid][4] = y * m;
+      a.dqc[rr] = dq;
+      a.actc[rr] = at;
+    } else {
+      part[tid][0] = part[tid][1] = part[tid][2] = part[tid][3] = part[tid][4] = 0.0f;
+    }
+    dqs[tid] = dq;
+    acts[tid] = at;
+  }
+  for (int e = tid; e < 16 * A; e += 256) {   // the Q values the actor's baseline uses (coma_learner.py:126)
+    const int i = e / A, aa = e - i * A;
+    if (r0 + i < R) a.qvals[((int64_t)t * R + r0 + i) * A + aa] = Qs[i * (A16 + 1) + aa];
+  }
+  __syncthreads();
+  if (tid < 5) {
+    float s = 0.0f;
+    for (int i = 0; i < 16; ++i) s += part[i][tid];
+    a.cpart[blockIdx.x * 8 + tid] = s;
+  }
+  // dH2 = dQ W3 o [H2 > 0] (dQ is one-hot at the taken action)
+  for (int e = tid; e < 16 * CH; e += 256) {
+    const int i = e >> 7, u = e & 127;
+    const float h2 = H2s[i * CP + u];
+    const float v = h2 > 0.0f ? dqs[i] * W3s[acts[i] * CP + u] : 0.0f;
+    dHs[i * CP + u] = v;
+    if (r0 + i < R) {
+      a.dH2c[(int64_t)(r0 + i) * CH + u] = v;
+      a.H2c[(int64_t)(r0 + i) * CH + u] = h2;
+    }
+  }
+  __syncthreads();
+  // dH1 = dH2 W2 o [H1 > 0]: B[kk][j] = W2[kk][j]
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int jt = w + 4 * jj;
+    f32x4 acc = {0, 0, 0, 0};
+    for (int k = 0; k < CH; k += 4) acc = mfma_f32_16x4(dHs[c * CP + k + g], W2s[(k + g) * CP + 16 * jt + c], acc);
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int i = 4 * g + reg, j = 16 * jt + c;
+      if (r0 + i < R) a.dH1c[(int64_t)(r0 + i) * CH + j] = H1s[i * CP + j] > 0.0f ? acc[reg] : 0.0f;
+    }
+  }
+}
+
+// wgrad: every critic gradient element of step t on MFMA, one writer each, per-block sums of squares for the norm.
+// A block owns 16 output rows (units, or actions for fc3) x 64 columns; wave w 16 of those columns; K = the R rows
+// of the step. The bias gradient is the column one past the weight's last (its B operand is the constant 1), so
+// every reduction over rows runs in the same MFMA order and no block loops over rows on its own.
+//   blocks [0, 8 N1)              dW1 | db1   (B = X_t, N1 = ceil((Kc + 1) / 64) column tiles)
+//   blocks [8 N1, 8 N1 + 24)      dW2 | db2   (B = H1)
+//   blocks [.., + 3 A16 / 16)     dW3 | db3   (A = dQ, one-hot at the taken action; B = H2)
+//   last block                    the step's bookkeeping
+__host__ __device__ inline int wgrad_blocks(const CDims& d) {
+  const int N1 = (d.Kc + 1 + 63) / 64, A16 = (d.A + 15) / 16 * 16;
+  return 8 * N1 + 24 + 3 * (A16 / 16) + 1;
+}
+
+__global__ __launch_bounds__(256) void coma_wgrad_kernel(CritArgs a, int t) {
+  if (!(a.msum[t] > 0.0f)) return;
+  const int R = a.d.R, Kp = a.d.Kp, Kc = a.d.Kc, A = a.d.A;
+  const int N1 = (Kc + 1 + 63) / 64, A16 = (A + 15) / 16 * 16;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
+  const int bid = blockIdx.x;
+  __shared__ float redsq[4];
+  float sq = 0.0f;
+  const int nb1 = 8 * N1, nb2 = nb1 + 24, nb3 = nb2 + 3 * (A16 / 16);
+  if (bid < nb3) {
+    int kind, u0, j0;
+    if (bid < nb1) { kind = 1; u0 = 16 * (bid / N1); j0 = 64 * (bid % N1); }
+    else if (bid < nb2) { kind = 2; u0 = 16 * ((bid - nb1) / 3); j0 = 64 * ((bid - nb1) % 3); }
+    else { kind = 3; u0 = 16 * ((bid - nb2) / 3); j0 = 64 * ((bid - nb2) % 3); }
+    const float* Bop = kind == 1 ? a.X + (int64_t)t * R * Kp : (kind == 2 ? a.H1c : a.H2c);
+    const int ldb = kind == 1 ? Kp : CH, ncol = kind == 1 ? Kc : CH;
+    const int nrow = kind == 3 ? A : CH;
+    const int64_t o_w = kind == 1 ? a.o_w1 : (kind == 2 ? a.o_w2 : a.o_w3);
+    const int64_t o_b = kind == 1 ? a.o_b1 : (kind == 2 ? a.o_b2 : a.o_b3);
+    const float* dH = kind == 1 ? a.dH1c : a.dH2c;
+    const int jc = j0 + 16 * w + c, u = u0 + c;
+    f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+    auto opA = [&](int rr) -> float {
+      if (rr >= R) return 0.0f;
+      if (kind == 3) return a.actc[rr] == u ? a.dqc[rr] : 0.0f;
+      return dH[(int64_t)rr * CH + u];
+    };
+    auto opB = [&](int rr) -> float {
+      if (rr >= R) return 0.0f;
+      return jc < ncol ? Bop[(int64_t)rr * ldb + jc] : (jc == ncol ? 1.0f : 0.0f);
+    };
+    int r = 0;
+    for (; r + 8 <= R; r += 8) {
+      const float a0 = opA(r + g), b0 = opB(r + g), a1 = opA(r + 4 + g), b1 = opB(r + 4 + g);
+      acc0 = mfma_f32_16x4(a0, b0, acc0);
+      acc1 = mfma_f32_16x4(a1, b1, acc1);
+    }
+    for (; r < R; r += 4) acc0 = mfma_f32_16x4(opA(r + g), opB(r + g), acc0);
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int row = u0 + 4 * g + reg;
+      const float v = acc0[reg] + acc1[reg];
+      if (row < nrow && jc <= ncol) {
+        if (jc < ncol) a.G[o_w + (int64_t)row * ncol + jc] = v;
+        else a.G[o_b + row] = v;
+        sq = fmaf(v, v, sq);
+      }
+    }
+  } else if (tid == 0) {
+    float* rec = a.crec + t * 8;
+    for (int k = 0; k < 5; ++k) {
+      float s = 0.0f;
+      for (int i = 0; i < a.nhead; ++i) s += a.cpart[i * 8 + k];
+      rec[k] = s;
+    }
+    rec[6] = 1.0f;
+    a.G[a.Pc] = a.msum[t];   // normaliser of the pending update
+    a.cstate[0] += 1;
+    a.cstate[1] = t;
+  }
+  sq = wave_sum(sq);
+  if (lane == 0) redsq[w] = sq;
+  __syncthreads();
+  if (tid == 0) a.cnorm[bid] = (redsq[0] + redsq[1]) + (redsq[2] + redsq[3]);
+}
+
+// The last live step's update over every critic parameter (after the reversed-t loop), into the caller's buffers
+// (in place when the last version already lives there: each element is read and written by one thread). The
+// clipped gradient stays in G, as .grad holds the last critic step's after the reference's train().
+__global__ __launch_bounds__(256) void coma_capply_kernel(CritArgs a) {
+  const int L = a.cstate[0];
+  if (L <= 0) return;
+  __shared__ float sh[4];
+  crit_coef(a, sh);
+  __syncthreads();
+  const float inv = sh[0], coef = sh[1];
+  const int src = (L - 1) & 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.crec[a.cstate[1] * 8 + 5] = sh[2];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.Pc; i += (int64_t)gridDim.x * 256) {
+    const float g = (a.G[i] * inv) * coef;
+    const float v = a.SQ[src][i] * a.hp.alpha + (1.0f - a.hp.alpha) * (g * g);
+    a.P[0][i] = a.P[src][i] + (-a.hp.lr) * (g / (sqrtf(v) + a.hp.eps));
+    a.SQ[0][i] = v;
+    a.G[i] = g;
+  }
+}
+
+// ----------------------------------------------------------------------------------------------- actor
+// One wave per (t, row), lanes = actions: BasicMAC.forward's pi_logits branch (basic_controller.py:53-73) and the
+// learner's renormalised masked policy, counterfactual baseline, advantage and log-pi term (coma_learner.py:59-77),
+// and the backward of sum(adv log pi m) down to the logits (unnormalised: the apply divides by sum m).
+// Writes dL [RT][Ap] (pad columns zero), pi [RT][A], per-block sums:
+// [0] -sum adv log pi m, [1] sum m, [2] sum adv m, [3] sum max(pi) m.
+__global__ __launch_bounds__(256) void coma_policy_kernel(Dims d, Rep rp, const float* __restrict__ logits,
+                                                          const float* __restrict__ qvals, float eps, float omeps,
+                                                          int mbs,
+                                                          int Ap, float* __restrict__ dL, float* __restrict__ pi_out,
+                                                          float* __restrict__ part) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t tr = (int64_t)blockIdx.x * 4 + wv;
+  const int A = d.A, n = d.n;
+  const int64_t RT = d.RT();
+  __shared__ float red[4][4];
+  float s_loss = 0.0f, s_m = 0.0f, s_adv = 0.0f, s_pmax = 0.0f;
+  if (tr < RT) {
+    const int t = (int)fdiv((uint32_t)tr, d.dR), r = (int)(tr - (int64_t)t * d.R);
+    const int b = (int)fdiv((uint32_t)r, d.dN), ag = r - b * n;
+    const int64_t slot = rp.ep(b) * d.t_stride + t;
+    const bool on = lane < A;
+    const int av = on ? rp.avail[(slot * n + ag) * A + lane] : 0;
+    float l = on ? logits[tr * A + lane] : -INFINITY;
+    if (mbs && on && !av) l = -1e10f;
+    const float mx = wave_max(l);
+    const float ex = on ? expf(l - mx) : 0.0f;
+    const float sm = ex / wave_sum(ex);
+    const float nact = mbs ? wave_sum(av ? 1.0f : 0.0f) : (float)A;
+    float out = on ? omeps * sm + eps / nact : 0.0f;
+    if (!av) out = 0.0f;                                   // mac_out[avail == 0] = 0
+    const float s = wave_sum(out);
+    const float p = (av && s > 0.0f) ? out / s : 0.0f;     // renormalise; 0/0 rows -> 0 (coma_learner.py:60-62)
+    const float qv = on ? qvals[tr * A + lane] : 0.0f;
+    const float baseline = wave_sum(p * qv);
+    const int at = (int)rp.actions[slot * n + ag];
+    const float q_taken = __shfl(qv, at, 64);
+    const float m = coma_mask(rp, slot, t);
+    const float pt = m == 0.0f ? 1.0f : __shfl(p, at, 64);
+    const float adv = q_taken - baseline;
+    const float lp = logf(pt);
+    const float pmax = wave_max(on ? p : -INFINITY);
+    s_loss = -(adv * lp) * m; s_m = m; s_adv = adv * m; s_pmax = pmax * m;
+    // backward of -sum adv log pi m (unnormalised) down to the logits
+    const float dpt = m == 0.0f ? 0.0f : (-(adv * m)) / pt;
+    const float dp = (av && lane == at) ? dpt : 0.0f;
+    const float dout = (av && s > 0.0f) ? (dp - dpt * pt) / s : 0.0f;
+    const float dsm = omeps * dout;
+    float dl = sm * (dsm - wave_sum(sm * dsm));
+    if (mbs && !av) dl = 0.0f;
+    if (lane < Ap) dL[tr * Ap + lane] = on ? dl : 0.0f;
+    if (on) pi_out[tr * A + lane] = p;
+  }
+  if (lane == 0) { red[wv][0] = s_loss; red[wv][1] = s_m; red[wv][2] = s_adv; red[wv][3] = s_pmax; }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    const int k = threadIdx.x;
+    part[(int64_t)blockIdx.x * 8 + k] = k < 4 ? ((red[0][k] + red[1][k]) + (red[2][k] + red[3][k])) : 0.0f;
+  }
+}
+
+// dHo = dL W2: the output-layer gradient entering the BPTT chain, [RT][64] (K = n_actions).
+struct DhoProb {
+  static constexpr int BN = 64;
+  const float* dL;   // [M][Ap]
+  int Ap, A;
+  const float* W2;   // [A][H]
+  float* dHo;        // [M][H]
+  int64_t M;
+  using APat = KPat;
+  using BPat = MPat;
+  static constexpr bool kRowSum = false;
+  struct Ctx {
+    const float* arow;
+  };
+  MQ_DEV Ctx make_ctx(int m0, int, int, int tid) const {
+    const int64_t m = m0 + KPat::row(tid);
+    return Ctx{m < M ? dL + m * Ap : nullptr};
+  }
+  MQ_DEV void krange(int, int& kb, int& ke) const { kb = 0; ke = A; }
+  MQ_DEV void load_a(const Ctx& c, int k0, int, float (&r)[4]) const {
+    const int k = k0 + KPat::kq(threadIdx.x);
+    ld4((c.arow && k < Ap) ? c.arow + k : nullptr, r);
+  }
+  MQ_DEV void load_b(const Ctx&, int, int k0, int ke, float (&r)[4]) const {
+    const int nn = MPat::row(threadIdx.x), k = k0 + MPat::kq(threadIdx.x);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = k + i < ke ? W2[(int64_t)(k + i) * H + nn] : 0.0f;
+  }
+  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int, int lane) const {
+    for_tile(acc, mrow0, ncol0, lane, [&](int m, int j, float v) {
+      if (m < M) dHo[(int64_t)m * H + j] = v;
+    });
+  }
+  MQ_DEV void rowsum_out(int, int, float) const {}
+};
+
+// [dW2 | db2] slab = dL^T Hs over rows tr (split-K), fc2 of rnn_agent.py:35.
+struct Dw2Prob {
+  static constexpr int BN = 64;
+  const float* dL;   // [K][Ap]
+  int Ap, A;
+  const float* Hs;   // [K][H] online hidden states
+  float* slab;       // [nsplit][A*H + A]
+  int64_t K;
+  int nsplit;
+  using APat = MPat;
+  using BPat = MPat;
+  static constexpr bool kRowSum = true;
+  struct Ctx {
+    int dummy;
+  };
+  MQ_DEV Ctx make_ctx(int, int, int, int) const { return Ctx{0}; }
+  MQ_DEV void krange(int z, int& kb, int& ke) const { krange_split((int)K, nsplit, z, kb, ke); }
+  MQ_DEV void load_a(const Ctx&, int k0, int ke, float (&r)[4]) const {
+    const int aa = MPat::row(threadIdx.x), k = k0 + MPat::kq(threadIdx.x);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = (aa < A && k + i < ke) ? dL[(int64_t)(k + i) * Ap + aa] : 0.0f;
+  }
+  MQ_DEV void load_b(const Ctx&, int, int k0, int ke, float (&r)[4]) const {
+    const int j = MPat::row(threadIdx.x), k = k0 + MPat::kq(threadIdx.x);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = (k + i < ke) ? Hs[(int64_t)(k + i) * H + j] : 0.0f;
+  }
+  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int z, int lane) const {
+    float* out = slab + (int64_t)z * (A * H + A);
+    for_tile(acc, mrow0, ncol0, lane, [&](int aa, int j, float v) {
+      if (aa < A) out[(int64_t)aa * H + j] = v;
+    });
+  }
+  MQ_DEV void rowsum_out(int aa, int z, float v) const {
+    if (aa < A) slab[(int64_t)z * (A * H + A) + A * H + aa] = v;
+  }
+};
+
+// Final stats (coma_learner.py:85-96): means of the per-step critic stats over the live steps in the order the
+// reference logs them (reversed t), then the actor's stats from the agent apply (stats[8..11] scratch on entry).
+__global__ void coma_stats_kernel(const float* __restrict__ crec, int T, const int* __restrict__ cstate,
+                                  float* __restrict__ stats) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s[5] = {0, 0, 0, 0, 0};
+  int cnt = 0;
+  for (int t = T - 1; t >= 0; --t) {
+    const float* rec = crec + t * 8;
+    if (rec[6] == 0.0f) continue;
+    const double msum = rec[1];
+    s[0] += (double)(rec[0] / rec[1]);
+    s[1] += (double)rec[5];
+    s[2] += (double)rec[2] / msum;
+    s[3] += (double)rec[3] / msum;
+    s[4] += (double)rec[4] / msum;
+    ++cnt;
+  }
+  // the agent apply_kernel wrote [loss, norm, sums[2]/msum, sums[3]/msum, sums[4]/msum, msum, coef, 0] at stats + 8
+  const float a_loss = stats[8], a_norm = stats[9], a_adv = stats[10], a_pmax = stats[11], a_msum = stats[13];
+  for (int k = 0; k < 5; ++k) stats[k] = cnt ? (float)(s[k] / cnt) : 0.0f;
+  stats[5] = a_adv;
+  stats[6] = a_loss;
+  stats[7] = a_norm;
+  stats[8] = a_pmax;
+  stats[9] = (float)cstate[0];
+  stats[10] = a_msum;
+}
+
+// BasicMAC.forward's pi_logits post-processing on the rollout side (basic_controller.py:53-73), in place.
+__global__ __launch_bounds__(256) void mc_policy_kernel(float* __restrict__ x, const int32_t* __restrict__ avail,
+                                                        int rows, int A, float eps, int mbs, int test_mode) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + wv;
+  if (row >= rows) return;
+  const bool on = lane < A;
+  const int av = on ? avail[(int64_t)row * A + lane] : 0;
+  float l = on ? x[(int64_t)row * A + lane] : -INFINITY;
+  if (mbs && on && !av) l = -1e10f;
+  const float mx = wave_max(l);
+  const float ex = on ? expf(l - mx) : 0.0f;
+  float p = ex / wave_sum(ex);
+  if (!test_mode) {
+    const float nact = mbs ? wave_sum(av ? 1.0f : 0.0f) : (float)A;
+    p = (1.0f - eps) * p + (1.0f * eps) / nact;
+    if (mbs && !av) p = 0.0f;
+  }
+  if (on) x[(int64_t)row * A + lane] = p;
+}
+
+}  // namespace mq

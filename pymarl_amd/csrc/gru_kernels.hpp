@@ -203,7 +203,10 @@ struct BwdIn {
   int act;
 };
 
-template <int RW, int VAR = 0>
+// DY (COMA actor, coma_learner.py:70-81): the output-layer gradient enters as a dense per-row vector
+// w.dHo[t][row][64] = dLogits W2 for every step t < Tp, instead of dchosen * W2[a_t] for t < T; the fc2 grads are
+// then a separate GEMM (Dw2Prob) and the slab's fc2 part stays zero.
+template <int RW, int VAR = 0, bool DY = false>
 __global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
                                                       Work w, int64_t slab_len) {
   constexpr int RL = (RW + 3) / 4;
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const floa
       const int64_t tr = (int64_t)tc * R + rr[0];
       const float* src = q == 0   ? w.Hs + (tc > 0 ? tr - R : tr) * H + k
                          : q == 1 ? w.X1 + tr * H + k
-                         : q == 2 ? w.dch + (int64_t)td * R + rr[0]
+                         : q == 2 ? (DY ? w.dHo + tr * H + k : w.dch + (int64_t)td * R + rr[0])
                                   : (const float*)(arow[0] + (int64_t)tc * d.n);
       s[0].gr = w.Gates[tr * (4 * H) + q * H + k];
       s[0].hp = *src;
@@ -270,7 +273,7 @@ __global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const floa
       s[ii].gr = g[k]; s[ii].gz = g[H + k]; s[ii].gn = g[2 * H + k]; s[ii].ghn = g[3 * H + k];
       s[ii].hp = w.Hs[(tc > 0 ? tr - R : tr) * H + k];
       s[ii].x1 = w.X1[tr * H + k];
-      s[ii].dch = w.dch[(int64_t)td * R + rr[ii]];
+      s[ii].dch = DY ? w.dHo[tr * H + k] : w.dch[(int64_t)td * R + rr[ii]];
       s[ii].act = (int)arow[ii][(int64_t)tc * d.n];
     }
   };
@@ -290,9 +293,9 @@ __global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const floa
       const float g = cur[0].gr, aux = cur[0].hp;
       const float gr = quad_bcast<0>(g), gz = quad_bcast<1>(g), gn = quad_bcast<2>(g), ghn = quad_bcast<3>(g);
       const float hp = t > 0 ? quad_bcast<0>(aux) : 0.0f, x1 = quad_bcast<1>(aux);
-      const float dchv = (live && t < T) ? quad_bcast<2>(aux) : 0.0f;
+      const float dchv = (live && (DY || t < T)) ? quad_bcast<2>(aux) : 0.0f;
       const int a = __builtin_bit_cast(int, quad_bcast<3>(aux));
-      const float dh = carry[0] + dchv * w2_s[a * H + k];
+      const float dh = carry[0] + (DY ? dchv : dchv * w2_s[a * H + k]);
       if (k == 0 && q == 0) { dch_s[pb][0] = dchv; act_s[pb][0] = a; }
       const float dn = dh * (1.0f - gz);
       const float dz = dh * (hp - gn);
@@ -319,9 +322,9 @@ __global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const floa
       const float gn = live ? cur[ii].gn : 0.0f, ghn = live ? cur[ii].ghn : 0.0f;
       const float hp = (live && t > 0) ? cur[ii].hp : 0.0f, x1 = live ? cur[ii].x1 : 0.0f;
       float dh = carry[ii];
-      const float dchv = (live && t < T) ? cur[ii].dch : 0.0f;
+      const float dchv = (live && (DY || t < T)) ? cur[ii].dch : 0.0f;
       const int a = cur[ii].act;
-      dh += dchv * w2_s[a * H + k];
+      dh += DY ? dchv : dchv * w2_s[a * H + k];
       if (k == 0) { dch_s[pb][i] = dchv; act_s[pb][i] = a; }
       const float dn = dh * (1.0f - gz);
       const float dz = dh * (hp - gn);
@@ -370,7 +373,7 @@ __global__ __launch_bounds__(512) void gru_bwd_kernel(Dims d, Rep rp, const floa
     const int pb = t & 1;
     // fc2 grads: dW2[a][k] += dchosen * h_t[k]; (a, k) is owned by lane (k, q = a % 4), so no two lanes ever
     // update the same word. h_t was the h_{t-1} record of step t+1, kept in a register since accumulate(t+1).
-    if (t < T) {
+    if (!DY && t < T) {
 #pragma unroll
       for (int i = 0; i < RW; ++i) {
         const int a = act_s[pb][i];

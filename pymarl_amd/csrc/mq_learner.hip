@@ -221,10 +221,10 @@ struct RedBuilder {
   int b1 = 0, b2 = 0;
   float* tmp;
   explicit RedBuilder(float* t) : tmp(t) {}
-  void add(const float* src, int nslab, int64_t len, float* dst, bool sq) {
+  void add(const float* src, int nslab, int64_t len, float* dst, bool sq, int64_t pitch = 0) {
     if (len <= 0 || nslab <= 0) return;
     RedRegion& R = pl.r[pl.nr++];
-    R.src = src; R.dst = dst; R.len = len; R.nslab = nslab; R.sq = sq ? 1 : 0;
+    R.src = src; R.dst = dst; R.len = len; R.pitch = pitch > 0 ? pitch : len; R.nslab = nslab; R.sq = sq ? 1 : 0;
     // at most kRedZ groups, so pass 2 sums <= 16 partials per element with all loads in flight
     R.zc = (nslab + kRedZ - 1) / kRedZ;
     R.ng = (nslab + R.zc - 1) / R.zc;
@@ -643,3 +643,4 @@ int mq_phase_times(mq_handle* h, float* ms, int32_t cap, int32_t* n) {
 }
 
 }  // extern "C"
+#include "coma_host.hpp"

@@ -20,6 +20,7 @@ struct RedRegion {
   float* dst;
   float* tmp;
   int64_t len;
+  int64_t pitch;    // slab stride in src (>= len: a region may cover a prefix of each slab)
   int nslab, zc, ng, sq;
   int blk1, blk2;   // first block of this region in pass 1 / pass 2
 };
@@ -47,7 +48,7 @@ __global__ __launch_bounds__(256) void red_pass1_kernel(RedPlan pl) {
   float s = 0.0f;
   for (int zb = z0; zb < z1; zb += kRedZ) {
 #pragma unroll
-    for (int u = 0; u < kRedZ; ++u) v[u] = (zb + u < z1) ? R.src[(int64_t)(zb + u) * R.len + i] : 0.0f;
+    for (int u = 0; u < kRedZ; ++u) v[u] = (zb + u < z1) ? R.src[(int64_t)(zb + u) * R.pitch + i] : 0.0f;
 #pragma unroll
     for (int u = 0; u < kRedZ; ++u) s += v[u];
   }

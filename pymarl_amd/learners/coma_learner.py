@@ -1,0 +1,211 @@
+"""COMALearner: counterfactual multi-agent policy gradients (reference: src/learners/coma_learner.py:9-171),
+MI355X-native.
+
+Same constructor, `train(batch, t_env, episode_num)`, `_update_targets`, `cuda`, `save_models`, `load_models`, the
+nine logged stats and the critic-step-counted hard target update. All of train() — the critic's all-steps target
+pass, TD(lambda), the T sequential critic RMSprop steps, the actor's GRU unroll, the pi_logits policy, the
+counterfactual baseline and the policy-gradient BPTT, both clips and both RMSprop steps — is one launch sequence of
+hand-written HIP kernels (include/mc_coma.h, pymarl_amd/csrc/coma_kernels.hpp); torch only owns the buffers.
+There is no CPU path. One synchronisation per train(): the stats read-back the target update needs.
+
+Reference quirk kept on purpose: the actor reads `mac.action_selector.epsilon`, the value the last rollout call of
+select_actions left there (basic_controller.py:64-67).
+"""
+from __future__ import annotations
+
+import copy
+import ctypes
+
+import torch as th
+from torch.optim import RMSprop
+
+from .. import _lib
+from ..modules.critics.coma import COMACritic
+from ..modules.flat import pack, rebind
+from .q_learner import replay_view
+from ..components.episode_buffer import SampledBatch
+
+
+def make_coma_config(args, input_dim, max_batch, max_seq):
+    cfg = _lib.MCConfig()
+    cfg.n_agents = args.n_agents
+    cfg.n_actions = args.n_actions
+    cfg.obs_dim = int(input_dim - (args.n_actions if args.obs_last_action else 0) -
+                      (args.n_agents if args.obs_agent_id else 0))
+    st = getattr(args, "state_shape", 1)
+    cfg.state_dim = int(st if isinstance(st, int) else th.Size(st).numel())
+    cfg.rnn_hidden_dim = args.rnn_hidden_dim
+    cfg.obs_last_action = int(bool(args.obs_last_action))
+    cfg.obs_agent_id = int(bool(args.obs_agent_id))
+    cfg.mask_before_softmax = int(bool(getattr(args, "mask_before_softmax", True)))
+    cfg.gamma = args.gamma
+    cfg.td_lambda = args.td_lambda
+    cfg.lr = args.lr
+    cfg.critic_lr = args.critic_lr
+    cfg.optim_alpha = args.optim_alpha
+    cfg.optim_eps = args.optim_eps
+    cfg.grad_norm_clip = args.grad_norm_clip
+    cfg.max_batch = int(max_batch)
+    cfg.max_seq = int(max_seq)
+    return cfg
+
+
+class COMALearner:
+    def __init__(self, mac, scheme, logger, args):
+        self.args = args
+        self.n_agents = args.n_agents
+        self.n_actions = args.n_actions
+        self.mac = mac
+        self.logger = logger
+        self.last_target_update_step = 0
+        self.critic_training_steps = 0
+        self.log_stats_t = -self.args.learner_log_interval - 1
+        self.critic = COMACritic(scheme, args)
+        self.target_critic = copy.deepcopy(self.critic)
+        self.agent_params = list(mac.parameters())
+        self.critic_params = list(self.critic.parameters())
+        self.params = self.agent_params + self.critic_params
+        self.agent_optimiser = RMSprop(params=self.agent_params, lr=args.lr, alpha=args.optim_alpha,
+                                       eps=args.optim_eps)
+        self.critic_optimiser = RMSprop(params=self.critic_params, lr=args.critic_lr, alpha=args.optim_alpha,
+                                        eps=args.optim_eps)
+        dev = self.mac.agent.fc1.weight.device
+        self._agent, self.n_agent_params = pack([self.mac.agent], device=dev)
+        self._critic, self.n_critic_params = pack([self.critic], device=dev)
+        self._tcritic, _ = pack([self.target_critic], device=dev)
+        self._alloc_state(dev)
+        self._handle = None
+        self._handle_key = None
+        self._steps = 0
+
+    # -- buffers ---------------------------------------------------------------------------------------------
+    def _alloc_state(self, dev):
+        Pa, Pc = self.n_agent_params, self.n_critic_params
+        self._agrad = th.zeros(Pa + _lib.NSUMS, dtype=th.float32, device=dev)
+        self._asq = th.zeros(Pa, dtype=th.float32, device=dev)
+        self._cgrad = th.zeros(Pc + _lib.MC_NTAIL, dtype=th.float32, device=dev)
+        self._csq = th.zeros(Pc, dtype=th.float32, device=dev)
+        self._stats = th.zeros(_lib.MC_NSTATS, dtype=th.float32, device=dev)
+        self._relink()
+
+    def _relink(self):
+        """Point module params, .grad and both optimisers' square_avg at the flat buffers."""
+        rebind([self.mac.agent], self._agent)
+        rebind([self.critic], self._critic)
+        rebind([self.target_critic], self._tcritic)
+        self.mac.agent._flat = self._agent
+        self.critic._flat = self._critic
+        self.target_critic._flat = self._tcritic
+        for params, grad, sq, opt in ((self.agent_params, self._agrad, self._asq, self.agent_optimiser),
+                                      (self.critic_params, self._cgrad, self._csq, self.critic_optimiser)):
+            o = 0
+            for p in params:
+                n = p.numel()
+                p.grad = grad[o:o + n].view_as(p)
+                st = opt.state[p]
+                st["square_avg"] = sq[o:o + n].view_as(p)
+                st.setdefault("step", th.tensor(0.0))
+                o += n
+        self._handle = None
+
+    def _get_handle(self, batch):
+        T = batch.max_seq_length if not isinstance(batch, SampledBatch) else batch.source.max_seq_length
+        need_b = max(batch.batch_size, getattr(self.args, "batch_size", 1))
+        if self._handle is None or self._handle_key[0] < need_b or self._handle_key[1] < T:
+            cfg = make_coma_config(self.args, self.mac.agent.input_dim, need_b, T)
+            h = _lib.ComaHandle(cfg)
+            if h.agent_offsets[-1] != self.n_agent_params or h.critic_offsets[-1] != self.n_critic_params:
+                raise _lib.MQError("parameter layout mismatch: library ({}, {}) vs modules ({}, {})".format(
+                    h.agent_offsets[-1], h.critic_offsets[-1], self.n_agent_params, self.n_critic_params))
+            P = _lib.ptr
+            _lib.check(h.lib.mc_bind(h.h, P(self._agent), P(self._agrad), P(self._asq), P(self._critic),
+                                     P(self._tcritic), P(self._cgrad), P(self._csq), P(self._stats)))
+            self._handle, self._handle_key = h, (need_b, T)
+        return self._handle
+
+    # -- reference API ---------------------------------------------------------------------------------------
+    def train(self, batch, t_env: int, episode_num: int):
+        _lib.require_gpu(self._agent)
+        h = self._get_handle(batch)
+        rep, keep = replay_view(batch)
+        eps = float(self.mac.action_selector.epsilon)
+        _lib.check(h.lib.mc_train_step(h.h, ctypes.byref(rep), ctypes.c_float(eps), _lib.stream_ptr()))
+        del keep
+        st = self._stats.tolist()   # the one synchronisation per train(): stats + critic step count
+        steps = int(round(st[9]))
+        self.critic_training_steps += steps
+        self._steps += 1
+        for p in self.agent_params:
+            self.agent_optimiser.state[p]["step"] += 1
+        for p in self.critic_params:
+            self.critic_optimiser.state[p]["step"] += steps
+        self._last = dict(zip(_lib.COMA_STATS, st))
+        self._last_batch = (batch.batch_size, rep.t_len)
+
+        if (self.critic_training_steps - self.last_target_update_step) / self.args.target_update_interval >= 1.0:
+            self._update_targets()
+            self.last_target_update_step = self.critic_training_steps
+
+        if t_env - self.log_stats_t >= self.args.learner_log_interval:
+            for key in ["critic_loss", "critic_grad_norm", "td_error_abs", "q_taken_mean", "target_mean"]:
+                self.logger.log_stat(key, self._last[key], t_env)
+            self.logger.log_stat("advantage_mean", self._last["advantage_mean"], t_env)
+            self.logger.log_stat("coma_loss", self._last["coma_loss"], t_env)
+            self.logger.log_stat("agent_grad_norm", self._last["agent_grad_norm"], t_env)
+            self.logger.log_stat("pi_max", self._last["pi_max"], t_env)
+            self.log_stats_t = t_env
+
+    def _update_targets(self):
+        if self._critic.is_cuda and self._handle is not None:
+            _lib.check(self._handle.lib.mc_update_targets(self._handle.h, _lib.stream_ptr()))
+        else:
+            with th.no_grad():
+                self._tcritic.copy_(self._critic)
+        self.logger.console_logger.info("Updated target network")
+
+    def cuda(self):
+        dev = th.device("cuda", th.cuda.current_device())
+        for name in ("_agent", "_critic", "_tcritic", "_agrad", "_asq", "_cgrad", "_csq", "_stats"):
+            setattr(self, name, getattr(self, name).to(dev))
+        self._relink()
+
+    def save_models(self, path):
+        self.mac.save_models(path)
+        th.save(self.critic.state_dict(), "{}/critic.th".format(path))
+        th.save(self.agent_optimiser.state_dict(), "{}/agent_opt.th".format(path))
+        th.save(self.critic_optimiser.state_dict(), "{}/critic_opt.th".format(path))
+
+    def load_models(self, path):
+        ml = lambda s, loc: s  # noqa: E731
+        self.mac.load_models(path)
+        self.critic.load_state_dict(th.load("{}/critic.th".format(path), map_location=ml, weights_only=True))
+        # Not quite right but I don't want to save target networks (reference comment, coma_learner.py:167)
+        self.target_critic.load_state_dict(self.critic.state_dict())
+        for fname, opt, params, sq in (("agent_opt.th", self.agent_optimiser, self.agent_params, self._asq),
+                                       ("critic_opt.th", self.critic_optimiser, self.critic_params, self._csq)):
+            opt.load_state_dict(th.load("{}/{}".format(path, fname), map_location=ml, weights_only=True))
+            o = 0
+            for p in params:
+                n = p.numel()
+                st = opt.state.get(p, {})
+                if "square_avg" in st:
+                    sq[o:o + n].copy_(st["square_avg"].reshape(-1))
+                o += n
+        self._relink()
+
+    # -- extras (parity / diagnostics) -----------------------------------------------------------------------
+    def last_stats(self):
+        return dict(self._last)
+
+    def last_intermediate(self, which):
+        """0: the critic Q values the actor used, (B, T, n, A); 1: TD(lambda) targets (B, T, n); 2: pi (B, T, n, A)."""
+        B, Tp = self._last_batch
+        T, n, A = Tp - 1, self.n_agents, self.n_actions
+        cnt = ctypes.c_int64()
+        h = self._handle
+        _lib.check(h.lib.mc_copy_intermediate(h.h, which, None, ctypes.byref(cnt), None))
+        out = th.empty(cnt.value, dtype=th.float32, device=self._agent.device)
+        _lib.check(h.lib.mc_copy_intermediate(h.h, which, _lib.ptr(out), ctypes.byref(cnt), _lib.stream_ptr()))
+        if which == 1:
+            return out.view(T, B, n).permute(1, 0, 2)
+        return out.view(T, B, n, A).permute(1, 0, 2, 3)

@@ -73,3 +73,33 @@ def rel(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.abs(a - b).max() / max(1e-30, np.abs(b).max()))
+
+
+def make_coma_args(case, **over):
+    a = SN(n_agents=case.n, n_actions=case.A, state_shape=case.S, obs_shape=case.O, rnn_hidden_dim=64, lr=5e-4,
+           critic_lr=5e-4, optim_alpha=0.99, optim_eps=1e-5, grad_norm_clip=10.0, gamma=0.99, td_lambda=0.8,
+           target_update_interval=case.target_update_interval, learner_log_interval=0, obs_last_action=True,
+           obs_agent_id=True, agent="rnn", mac="basic_mac", agent_output_type="pi_logits",
+           action_selector="multinomial", epsilon_start=0.5, epsilon_finish=0.01, epsilon_anneal_time=100000,
+           mask_before_softmax=case.mask_before_softmax, batch_size=case.B, learner="coma_learner", device="cuda",
+           use_cuda=True)
+    for k, v in over.items():
+        setattr(a, k, v)
+    return a
+
+
+def build_coma(case, device="cuda", **over):
+    args = make_coma_args(case, **over)
+    groups = {"agents": case.n}
+    preprocess = {"actions": ("actions_onehot", [OneHot(out_dim=case.A)])}
+    buf = ReplayBuffer(make_scheme(case), groups, case.n_episodes, case.T + 1, preprocess=preprocess, device=device)
+    buf.load_arrays(case.data)
+    mac = mac_REGISTRY["basic_mac"](buf.scheme, groups, args)
+    logger = Logger(logging.getLogger("mc-test"))
+    learner = le_REGISTRY["coma_learner"](mac, buf.scheme, logger, args)
+    learner.cuda()
+    mac.agent.load_state_dict({k: th.from_numpy(v) for k, v in case.agent_params.items()})
+    cd = {k: th.from_numpy(v) for k, v in case.critic_params.items()}
+    learner.critic.load_state_dict(cd)
+    learner.target_critic.load_state_dict(cd)
+    return args, buf, mac, learner, logger

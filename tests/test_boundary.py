@@ -11,18 +11,18 @@ import pytest
 from pymarl_amd import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "mq_learner.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("mq_learner.h", "mc_coma.h")]
 
 
 def declared_functions():
-    text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(mq_\w+)\s*\(", text, flags=re.M)))
+    text = "".join(open(h).read() for h in HEADERS)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(m[qc]_\w+)\s*\(", text, flags=re.M)))
 
 
 def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     decl = declared_functions()
-    assert len(decl) >= 15
+    assert len(decl) >= 23
     for name in decl:
         assert hasattr(lib, name), name
     assert sorted(_lib.EXPORTS) == decl
@@ -33,11 +33,13 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
     src.write_text("""
 #include <stdio.h>
 #include <stddef.h>
-#include "mq_learner.h"
+#include "mc_coma.h"
 int main(void) {
   printf("%zu %zu %zu %zu %zu\\n", sizeof(mq_config), offsetof(mq_config, gamma), offsetof(mq_config, max_seq),
          sizeof(mq_replay), offsetof(mq_replay, batch_size));
   printf("%d %d\\n", MQ_P_COUNT, MQ_NSUMS);
+  printf("%zu %zu %zu %d %d %d\\n", sizeof(mc_config), offsetof(mc_config, gamma), offsetof(mc_config, max_seq),
+         MC_P_COUNT, MC_NTAIL, MC_NSTATS);
   return 0;
 }
 """)
@@ -46,7 +48,9 @@ int main(void) {
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
     c = [int(x) for x in out]
     py = [ctypes.sizeof(_lib.MQConfig), _lib.MQConfig.gamma.offset, _lib.MQConfig.max_seq.offset,
-          ctypes.sizeof(_lib.MQReplay), _lib.MQReplay.batch_size.offset, _lib.P_COUNT, _lib.NSUMS]
+          ctypes.sizeof(_lib.MQReplay), _lib.MQReplay.batch_size.offset, _lib.P_COUNT, _lib.NSUMS,
+          ctypes.sizeof(_lib.MCConfig), _lib.MCConfig.gamma.offset, _lib.MCConfig.max_seq.offset, _lib.MC_P_COUNT,
+          _lib.MC_NTAIL, _lib.MC_NSTATS]
     assert c == py
 
 
