@@ -1,6 +1,6 @@
 """Learner throughput bench: QLearner.train on synthetic replay, MI355X, 1..8 GPUs (one process per GPU).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
 
 Metric (BASELINE.json): learner samples/s = B*T*n_agents per train() / wall seconds, whole job (all ranks).
@@ -198,6 +198,93 @@ def cpu_baseline(cfg_name, data, budget_s=12.0):
                       f"median {s * 1e3:.1f} ms/step, {cores} BLAS threads"}
 
 
+def coma_cpu_baseline(cfg_name, data, budget_s=12.0):
+    """Time the numpy COMA oracle's train() (oracle/coma_np.py) on this host's cores (bounded sample)."""
+    from oracle.coma_np import OracleCOMALearner, critic_input_dim, critic_param_shapes
+    from pymarl_amd.utils.synthetic import agent_param_shapes, init_params
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    _, n, A, O, S, T, B, _ = CONFIGS[cfg_name]
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    cfg = dict(n_agents=n, n_actions=A, gamma=0.99, td_lambda=0.8, lr=5e-4, critic_lr=5e-4, optim_alpha=0.99,
+               optim_eps=1e-5, grad_norm_clip=10.0, target_update_interval=200, mask_before_softmax=False)
+    o = OracleCOMALearner(init_params(agent_param_shapes(O + A + n, 64, A), 1),
+                          init_params(critic_param_shapes(critic_input_dim(n, A, O, S), A), 201), cfg)
+    rng = np.random.RandomState(7)
+    ctx = threadpool_limits(limits=cores) if threadpool_limits else None
+    times = []
+    t_start = time.perf_counter()
+    while True:
+        ids = rng.choice(len(data["obs"]), B, replace=False)
+        batch = {k: v[ids] for k, v in data.items()}
+        t0 = time.perf_counter()
+        o.train(batch, 0, len(times), 0.3)
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > budget_s and len(times) >= 2:
+            break
+    del ctx
+    s = float(np.median(times))
+    return {"value": B * T * n / s, "unit": "samples/s", "cores": cores, "kind": "port",
+            "sample": f"{len(times)} numpy-oracle COMA train() steps of {cfg_name} (B={B}, T={T}, n={n}), "
+                      f"median {s * 1e3:.1f} ms/step, {cores} BLAS threads"}
+
+
+def coma_bench(a):
+    """cfg5: COMALearner.train on one GPU (the critic's T-step chain is a per-step exchange; DP COMA would need T
+    all-reduces per train, SURVEY.md §8e, and is not built: this line is N = 1)."""
+    import torch as th
+    device = th.device("cuda", 0)
+    th.cuda.set_device(device)
+    args, buf, learner, data, mac = build_coma_workload(a.config, device)
+    _, n, A, O, S, T, B, desc = CONFIGS[a.config]
+    np.random.seed(2)
+
+    def step(k):
+        b = buf.sample(B)
+        mac.action_selector.epsilon = mac.action_selector.schedule.eval(1000 * k)
+        learner.train(b[:, :b.max_t_filled()], 1000 * k, 8 * k)
+
+    for k in range(max(1, a.warmup)):
+        step(k)
+    th.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        step(k)
+    th.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    learner.set_timing(True)
+    chains = []
+    for k in range(min(a.steps, 20)):
+        step(k)
+        chains.append(learner.phase_times())
+    learner.set_timing(False)
+    chain_ms = float(np.mean([c["critic_chain"] for c in chains]))
+    Kc = S + O + 2 * n * A + n
+    R = B * n
+    step_flops = 2 * R * (2 * Kc * 128 + 3 * 128 * 128 + 2 * 128 * A)   # one critic step, fwd + bwd (DESIGN.md)
+    achieved = step_flops / (chain_ms * 1e-3 / T) / 1e12
+    value = B * T * n * a.steps / dt
+    cpu = None if a.no_cpu_baseline else coma_cpu_baseline(a.config, data)
+    line = {
+        "metric": METRIC, "value": value, "unit": "samples/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32", "data": "synthetic (SURVEY.md §8d replay recipe, random-init weights)",
+        "config": {"workload": desc, "learner": "coma_learner", "n_agents": n, "n_actions": A, "obs_dim": O,
+                   "state_dim": S, "episode_limit": T, "batch_per_gpu": B, "global_batch": B,
+                   "replay_episodes": buf.buffer_size, "parallelism": "dp1"},
+        "roofline": {"bound": "mfma", "kernel": "critic step chain (l1 + head + wgrad, x T)",
+                     "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "launch_ms": chain_ms / T,
+                     "flops_per_launch": step_flops,
+                     "phases_ms": {k: float(np.mean([c[k] for c in chains])) for k in chains[0]}},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line))
+
+
 def pmc_traffic(cfg_name, phase):
     """HBM bytes per launch of `phase` from a committed PMC summary (profiles/*pmc*.json), else None."""
     import glob
@@ -222,6 +309,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--phases", action="store_true", help="print every phase's mean ms to stderr")
     a = ap.parse_args()
+    if a.config == "cfg5":
+        return coma_bench(a)
 
     import torch as th
     import torch.distributed as dist

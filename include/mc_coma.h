@@ -60,6 +60,11 @@ int mc_update_targets(mc_handle* h, void* stream);
  * unless test_mode the epsilon floor (+ zeroing when mask_before_softmax). avail [rows][n_actions] int32. */
 int mc_policy(float* logits, const int32_t* avail, int32_t rows, int32_t n_actions, float epsilon,
               int32_t mask_before_softmax, int32_t test_mode, void* stream);
+/* Optional HIP-event timing of train steps (bench / profiling): on != 0 records events around the critic's
+ * target pass + TD(lambda), the T-step critic chain, and the actor part of every following mc_train_step;
+ * mc_phase_times writes the last step's [prologue, critic chain, actor] ms (synchronises on the events). */
+int mc_set_timing(mc_handle* h, int32_t on);
+int mc_phase_times(mc_handle* h, float* ms /* [3] */);
 /* 0 = critic Q values the actor used [T][B*n][A]; 1 = TD(lambda) targets [T][B*n]; 2 = policy pi [T][B*n][A]. */
 int mc_copy_intermediate(mc_handle* h, int which, float* dst, int64_t* count, void* stream);
 

@@ -28,7 +28,7 @@ EXPORTS = [
     "mq_greedy_actions", "mq_set_timing", "mq_phase_times", "mq_phase_names", "mq_set_data_parallel",
     # include/mc_coma.h
     "mc_create", "mc_destroy", "mc_param_offsets", "mc_bind", "mc_train_step", "mc_update_targets", "mc_policy",
-    "mc_copy_intermediate",
+    "mc_copy_intermediate", "mc_set_timing", "mc_phase_times",
 ]
 
 MC_P_COUNT = 6
@@ -118,6 +118,8 @@ def load(required=True):
         "mc_update_targets": ([vp, vp], ctypes.c_int),
         "mc_policy": ([vp, vp, i32, i32, ctypes.c_float, i32, i32, vp], ctypes.c_int),
         "mc_copy_intermediate": ([vp, ctypes.c_int, vp, ctypes.POINTER(i64), vp], ctypes.c_int),
+        "mc_set_timing": ([vp, i32], ctypes.c_int),
+        "mc_phase_times": ([vp, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -22,6 +22,8 @@ struct mc_handle {
   // actor workspace
   float *dL, *dHo, *pi, *ppart, *slab_fc2, *red_tmp, *norm_part;
   int last_T = 0, last_R = 0;
+  bool timing = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 namespace {
@@ -116,6 +118,8 @@ int mc_create(const mc_config* cfg, mc_handle** out) {
 int mc_destroy(mc_handle* h) {
   if (!h) return MQ_OK;
   if (h->ws) (void)hipFree(h->ws);
+  for (auto& e : h->ev)
+    if (e) (void)hipEventDestroy(e);
   mq_destroy(h->ah);
   delete h;
   return MQ_OK;
@@ -159,6 +163,7 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   cd.dR = make_fastdiv((uint32_t)R);
   cd.dN = make_fastdiv((uint32_t)n);
 
+  if (h->timing) MQ_HIP(hipEventRecord(h->ev[0], s));
   MQ_HIP(hipMemsetAsync(h->crec, 0, (size_t)T * 8 * sizeof(float), s));
   MQ_HIP(hipMemsetAsync(h->cstate, 0, 4 * sizeof(int), s));
   hipLaunchKernelGGL(coma_mask_kernel, dim3((T + 255) / 256), dim3(256), 0, s, cd, rp, h->msum);
@@ -197,6 +202,7 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   if (lds_l1 > 160 * 1024 || lds_head > 160 * 1024)
     return set_err(MQ_ERR_ARG, "critic input width or n_actions too large for the LDS-staged critic step");
   MQ_HIP(hipMemsetAsync(h->qvals, 0, (size_t)T * R * A * sizeof(float), s));   // skipped steps keep q_vals = 0
+  if (h->timing) MQ_HIP(hipEventRecord(h->ev[1], s));
   for (int t = T - 1; t >= 0; --t) {
     hipLaunchKernelGGL(coma_l1_kernel, dim3(ca.nhead, CH / 16), dim3(256), lds_l1, s, ca, t);
     hipLaunchKernelGGL(coma_head_kernel, dim3(ca.nhead), dim3(256), lds_head, s, ca, t);
@@ -207,6 +213,7 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
                      ca);
   MQ_HIP(hipGetLastError());
 
+  if (h->timing) MQ_HIP(hipEventRecord(h->ev[2], s));
   // ---- actor: the agent unroll over t < T (coma_learner.py:52-57), online net only
   mq_replay av = *batch;
   av.t_len = T;
@@ -304,8 +311,25 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   hipLaunchKernelGGL(coma_stats_kernel, dim3(1), dim3(64), 0, s, (const float*)h->crec, T,
                      (const int*)h->cstate, h->stats);
   MQ_HIP(hipGetLastError());
+  if (h->timing) MQ_HIP(hipEventRecord(h->ev[3], s));
   h->last_T = T;
   h->last_R = R;
+  return MQ_OK;
+}
+
+int mc_set_timing(mc_handle* h, int32_t on) {
+  if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
+  for (auto& e : h->ev)
+    if (!e) MQ_HIP(hipEventCreate(&e));
+  h->timing = on != 0;
+  return MQ_OK;
+}
+
+int mc_phase_times(mc_handle* h, float* ms) {
+  if (!h || !ms) return set_err(MQ_ERR_ARG, "NULL argument");
+  if (!h->ev[3]) return set_err(MQ_ERR_STATE, "timing was never enabled");
+  MQ_HIP(hipEventSynchronize(h->ev[3]));
+  for (int i = 0; i < 3; ++i) MQ_HIP(hipEventElapsedTime(&ms[i], h->ev[i], h->ev[i + 1]));
   return MQ_OK;
 }
 

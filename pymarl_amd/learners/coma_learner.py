@@ -209,3 +209,13 @@ class COMALearner:
         if which == 1:
             return out.view(T, B, n).permute(1, 0, 2)
         return out.view(T, B, n, A).permute(1, 0, 2, 3)
+
+    def set_timing(self, on=True):
+        """HIP events around the critic prologue, the T-step critic chain and the actor of the following steps."""
+        _lib.check(self._handle.lib.mc_set_timing(self._handle.h, int(bool(on))))
+
+    def phase_times(self):
+        """{prologue, critic_chain, actor} ms of the last train() (synchronises)."""
+        ms = (ctypes.c_float * 3)()
+        _lib.check(self._handle.lib.mc_phase_times(self._handle.h, ms))
+        return {"prologue": ms[0], "critic_chain": ms[1], "actor": ms[2]}
