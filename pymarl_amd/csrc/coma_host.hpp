@@ -15,7 +15,7 @@ struct mc_handle {
         *cgrad = nullptr, *csq = nullptr, *stats = nullptr;
   void* ws = nullptr;
   // critic workspace
-  float *X, *H1t, *H2t, *Qt, *tgt, *msum, *H1c, *H2c, *dH1c, *dH2c, *dqc, *qvals, *cpart, *cnorm, *crec;
+  float *X, *H1t, *H2t, *Qt, *tgt, *msum, *H1p, *H1c, *H2c, *dH1c, *dH2c, *dqc, *qvals, *cpart, *cnorm, *crec;
   float *Pshadow, *SQshadow;
   int* actc;
   int* cstate;
@@ -79,6 +79,7 @@ int mc_create(const mc_config* cfg, mc_handle** out) {
       Tp * R * CH, Tp * R * CH,    // H1t, H2t
       Tp * R * A,                  // Qt
       T * R, T,                    // tgt, msum
+      (int64_t)l1_slices(h->Kp) * R * CH,   // H1p
       R * CH, R * CH, R * CH, R * CH,   // H1c H2c dH1c dH2c
       R, R,                        // dqc, actc
       T * R * A,                   // qvals
@@ -103,7 +104,7 @@ int mc_create(const mc_config* cfg, mc_handle** out) {
   float* b = (float*)h->ws;
   int k = 0;
   h->X = b + offs[k++]; h->H1t = b + offs[k++]; h->H2t = b + offs[k++]; h->Qt = b + offs[k++];
-  h->tgt = b + offs[k++]; h->msum = b + offs[k++];
+  h->tgt = b + offs[k++]; h->msum = b + offs[k++]; h->H1p = b + offs[k++];
   h->H1c = b + offs[k++]; h->H2c = b + offs[k++]; h->dH1c = b + offs[k++]; h->dH2c = b + offs[k++];
   h->dqc = b + offs[k++]; h->actc = (int*)(b + offs[k++]);
   h->qvals = b + offs[k++]; h->cpart = b + offs[k++]; h->cnorm = b + offs[k++]; h->crec = b + offs[k++];
@@ -181,7 +182,9 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
     CLinProb l3{h->H2t, CH, tc + h->coff[MC_P_FC3_W], tc + h->coff[MC_P_FC3_B], h->Qt, M, A, CH, 0};
     MQ_HIP(launch_gemm(l3, (int)M, A, 1, s));
   }
-  hipLaunchKernelGGL(coma_td_kernel, dim3((R + 63) / 64), dim3(64), 0, s, cd, rp, h->Qt, h->tgt);
+  const size_t lds_td = (size_t)Tp * (n + 3) * sizeof(float);
+  if (lds_td > 160 * 1024 || n > 256) return set_err(MQ_ERR_ARG, "episode too long for the LDS TD(lambda) pass");
+  hipLaunchKernelGGL(coma_td_kernel, dim3(batch->batch_size), dim3(256), lds_td, s, cd, rp, h->Qt, h->tgt);
   MQ_HIP(hipGetLastError());
 
   // the critic's T sequential steps (coma_learner.py:118-139)
@@ -190,22 +193,24 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   ca.P[0] = h->critic; ca.P[1] = h->Pshadow; ca.SQ[0] = h->csq; ca.SQ[1] = h->SQshadow; ca.G = h->cgrad;
   ca.o_w1 = h->coff[MC_P_FC1_W]; ca.o_b1 = h->coff[MC_P_FC1_B]; ca.o_w2 = h->coff[MC_P_FC2_W];
   ca.o_b2 = h->coff[MC_P_FC2_B]; ca.o_w3 = h->coff[MC_P_FC3_W]; ca.o_b3 = h->coff[MC_P_FC3_B]; ca.Pc = h->Pc;
-  ca.X = h->X; ca.tgt = h->tgt; ca.msum = h->msum; ca.H1c = h->H1c; ca.H2c = h->H2c; ca.dH1c = h->dH1c;
+  ca.X = h->X; ca.tgt = h->tgt; ca.msum = h->msum; ca.H1p = h->H1p; ca.KS = l1_slices(h->Kp); ca.H1c = h->H1c; ca.H2c = h->H2c; ca.dH1c = h->dH1c;
   ca.dH2c = h->dH2c; ca.dqc = h->dqc; ca.actc = h->actc; ca.qvals = h->qvals; ca.cpart = h->cpart;
   ca.cnorm = h->cnorm; ca.crec = h->crec; ca.cstate = h->cstate;
   ca.nhead = (R + 15) / 16;
   ca.nwgrad = wgrad_blocks(cd);
   ca.hp = OptHP{c.critic_lr, c.optim_alpha, c.optim_eps, c.grad_norm_clip, 1};
   const int A16 = (A + 15) / 16 * 16;
-  const size_t lds_l1 = ((size_t)2 * 16 * (h->Kp + 1) + 4 * 16 * 16) * sizeof(float);
+  const size_t lds_l1 = (size_t)(16 + kL1Rows) * (KW + 1) * sizeof(float);
   const size_t lds_head = ((size_t)(CH + A16 + 48) * (CH + 1) + 16 * (A16 + 1) + CH + A16) * sizeof(float);
   if (lds_l1 > 160 * 1024 || lds_head > 160 * 1024)
     return set_err(MQ_ERR_ARG, "critic input width or n_actions too large for the LDS-staged critic step");
   MQ_HIP(hipMemsetAsync(h->qvals, 0, (size_t)T * R * A * sizeof(float), s));   // skipped steps keep q_vals = 0
   if (h->timing) MQ_HIP(hipEventRecord(h->ev[1], s));
   for (int t = T - 1; t >= 0; --t) {
-    hipLaunchKernelGGL(coma_l1_kernel, dim3(ca.nhead, CH / 16), dim3(256), lds_l1, s, ca, t);
-    hipLaunchKernelGGL(coma_head_kernel, dim3(ca.nhead), dim3(256), lds_head, s, ca, t);
+    const int Lexp = T - 1 - t;   // live steps before t when none was skipped
+    hipLaunchKernelGGL(coma_l1_kernel, dim3(ca.KS, CH / 16, (R + kL1Rows - 1) / kL1Rows), dim3(256), lds_l1, s, ca, t,
+                       Lexp);
+    hipLaunchKernelGGL(coma_head_kernel, dim3(ca.nhead), dim3(kHeadThreads), lds_head, s, ca, t, Lexp);
     hipLaunchKernelGGL(coma_wgrad_kernel, dim3(ca.nwgrad), dim3(256), 0, s, ca, t);
   }
   MQ_HIP(hipGetLastError());

@@ -144,26 +144,42 @@ struct CLinProb {
   MQ_DEV void rowsum_out(int, int, float) const {}
 };
 
-// build_td_lambda_targets (rl_utils.py:4-14) for one (episode, agent) column per thread: the backward recursion
-// ret_t = lambda gamma ret_{t+1} + mask_t (r_t + (1 - lambda) gamma Q'_{t+1}(a_{t+1}) (1 - term_t)),
-// ret_{T} = Q'_T(a_T) (1 - sum_t term_t). Writes targets [T][R].
-__global__ __launch_bounds__(64) void coma_td_kernel(CDims d, Rep rp, const float* __restrict__ Qt,
-                                                     float* __restrict__ tgt) {
-  const int r = blockIdx.x * 64 + threadIdx.x;
-  if (r >= d.R) return;
-  const int b = (int)fdiv((uint32_t)r, d.dN), ag = r - b * d.n;
+// build_td_lambda_targets (rl_utils.py:4-14), one workgroup per episode: the recursion's inputs (the target critic's
+// Q at the taken action for every (t, agent), reward, terminated, mask) are gathered into LDS by all threads, then
+// one thread per agent runs the backward recursion out of LDS
+//   ret_T = Q'_T(a_T) (1 - sum_t term_t),
+//   ret_t = lambda gamma ret_{t+1} + mask_t (r_t + (1 - lambda) gamma Q'_{t+1}(a_{t+1}) (1 - term_t)),
+// in torch's evaluation order without FMA contraction. Writes targets [T][R]. LDS: Tp * (n + 3) floats.
+__global__ __launch_bounds__(256) void coma_td_kernel(CDims d, Rep rp, const float* __restrict__ Qt,
+                                                      float* __restrict__ tgt) {
+  extern __shared__ float sm[];
+  const int b = blockIdx.x, n = d.n, Tp = d.Tp;
+  float* tq = sm;              // [Tp][n]
+  float* rw = tq + Tp * n;     // [Tp]
+  float* om = rw + Tp;         // [Tp] 1 - terminated
+  float* mk = om + Tp;         // [Tp] mask
   const int64_t e0 = rp.ep(b) * d.t_stride;
-  auto taken = [&](int t) { return Qt[((int64_t)t * d.R + r) * d.A + (int)rp.actions[(e0 + t) * d.n + ag]]; };
+  for (int e = threadIdx.x; e < Tp * n; e += 256) {
+    const int t = e / n, ag = e - t * n;
+    const int r = b * n + ag;
+    tq[e] = Qt[((int64_t)t * d.R + r) * d.A + (int)rp.actions[(e0 + t) * n + ag]];
+  }
+  for (int t = threadIdx.x; t < Tp; t += 256) {
+    rw[t] = rp.reward[e0 + t];
+    om[t] = 1.0f - (float)rp.term[e0 + t];
+    mk[t] = coma_mask(rp, e0 + t, t);
+  }
+  __syncthreads();
+  const int ag = threadIdx.x;
+  if (ag >= n) return;
   float tsum = 0.0f;
-  for (int t = 0; t < d.T; ++t) tsum += (float)rp.term[e0 + t];
-  float ret = taken(d.Tp - 1) * (1.0f - tsum);
-  for (int t = d.Tp - 2; t >= 0; --t) {
-    const int64_t slot = e0 + t;
-    const float m = coma_mask(rp, slot, t);
-    // torch's evaluation order, no FMA contraction
-    const float inner = __fadd_rn(rp.reward[slot], __fmul_rn(__fmul_rn(d.og, taken(t + 1)), 1.0f - (float)rp.term[slot]));
-    ret = __fadd_rn(__fmul_rn(d.lg, ret), __fmul_rn(m, inner));
-    tgt[(int64_t)t * d.R + r] = ret;
+  for (int t = 0; t < d.T; ++t) tsum += 1.0f - om[t];
+  float ret = tq[(Tp - 1) * n + ag] * (1.0f - tsum);
+  float* out = tgt + b * n + ag;
+  for (int t = Tp - 2; t >= 0; --t) {
+    const float inner = __fadd_rn(rw[t], __fmul_rn(__fmul_rn(d.og, tq[(t + 1) * n + ag]), om[t]));
+    ret = __fadd_rn(__fmul_rn(d.lg, ret), __fmul_rn(mk[t], inner));
+    out[(int64_t)t * d.R] = ret;
   }
 }
 
@@ -179,6 +195,8 @@ struct CritArgs {
   const float* X;    // [Tp][R][Kp]
   const float* tgt;  // [T][R]
   const float* msum; // [T]
+  float* H1p;        // [KS][R][CH] l1's partial pre-activations, one per K slice
+  int KS;            // K slices of W1 (l1 grid.x)
   float* H1c;        // [R][CH] this step's activations / gradients
   float* H2c;
   float* dH1c;
@@ -228,18 +246,19 @@ constexpr int kStageB = 16;
 template <class Idx, class Put>
 MQ_DEV void crit_stage(const CritArgs& a, int N, bool pend, float inv, float coef, int src, int dst, bool owner,
                        Idx idx, Put put) {
-  for (int e0 = threadIdx.x; e0 < N; e0 += 256 * kStageB) {
+  const int nt = blockDim.x;
+  for (int e0 = threadIdx.x; e0 < N; e0 += nt * kStageB) {
     float gv[kStageB], sv[kStageB], pv[kStageB];
 #pragma unroll
     for (int u = 0; u < kStageB; ++u) {
-      const int e = e0 + 256 * u;
+      const int e = e0 + nt * u;
       const int64_t i = idx(e < N ? e : N - 1);
       pv[u] = a.P[src][i];
       if (pend) { gv[u] = a.G[i]; sv[u] = a.SQ[src][i]; }
     }
 #pragma unroll
     for (int u = 0; u < kStageB; ++u) {
-      const int e = e0 + 256 * u;
+      const int e = e0 + nt * u;
       if (e >= N) break;
       float p = pv[u];
       if (pend) {
@@ -257,85 +276,163 @@ MQ_DEV void crit_stage(const CritArgs& a, int N, bool pend, float inv, float coe
   }
 }
 
-// l1: H1 = relu(X_t W1^T + b1) for a 16-row x 16-unit tile; K split over the 4 waves.
-__global__ __launch_bounds__(256) void coma_l1_kernel(CritArgs a, int t) {
-  if (!(a.msum[t] > 0.0f)) return;
-  extern __shared__ float sm[];
-  const int Kp = a.d.Kp, KP = Kp + 1, Kc = a.d.Kc, R = a.d.R;
-  float* Ws = sm;               // [16][KP]
-  float* Xs = Ws + 16 * KP;     // [16][KP]
-  float* red = Xs + 16 * KP;    // [4][16][16]
-  __shared__ float sh[4];
-  __shared__ float bs[16];
-  const int tid = threadIdx.x, u0 = blockIdx.y * 16, r0 = blockIdx.x * 16;
+// Two-phase form of crit_stage for the largest region of a launch: the loads are issued before the clip coefficient
+// is known (it needs its own round trip to the norm partials), so both round trips overlap.
+template <int NE>
+struct StageRegs {
+  float p[NE], g[NE], s[NE];
+};
+
+template <int NE, class Idx>
+MQ_DEV void stage_load(const CritArgs& a, int N, bool pend, int src, Idx idx, StageRegs<NE>& r) {
+#pragma unroll
+  for (int u = 0; u < NE; ++u) {
+    const int e = threadIdx.x + blockDim.x * u;
+    const int64_t i = idx(e < N ? e : N - 1);
+    r.p[u] = a.P[src][i];
+    if (pend) { r.g[u] = a.G[i]; r.s[u] = a.SQ[src][i]; }
+  }
+}
+
+template <int NE, class Idx, class Put>
+MQ_DEV void stage_apply(const CritArgs& a, int N, bool pend, float inv, float coef, int dst, bool owner,
+                        const StageRegs<NE>& r, Idx idx, Put put) {
+#pragma unroll
+  for (int u = 0; u < NE; ++u) {
+    const int e = threadIdx.x + blockDim.x * u;
+    if (e >= N) break;
+    float p = r.p[u];
+    if (pend) {
+      const float g = (r.g[u] * inv) * coef;
+      const float v = r.s[u] * a.hp.alpha + (1.0f - a.hp.alpha) * (g * g);
+      p = p + (-a.hp.lr) * (g / (sqrtf(v) + a.hp.eps));
+      if (owner) {
+        const int64_t i = idx(e);
+        a.SQ[dst][i] = v;
+        a.P[dst][i] = p;
+      }
+    }
+    put(e, p);
+  }
+}
+
+constexpr int kHeadThreads = 1024;
+constexpr int KW = 176;        // W1 columns per l1 block: 44 MFMA k-steps
+constexpr int kL1Rows = 128;   // rows of X_t one l1 block stages (grid.z covers more)
+
+__host__ __device__ inline int l1_slices(int Kp) { return (Kp + KW - 1) / KW; }
+
+// l1: partial H1 pre-activations over one K slice: block (ks, ut, rc) owns W1[16 ut .. +16][KW ks .. +KW] — it is
+// the only block that stages, updates and writes back those weights — and multiplies them with rows
+// [128 rc, +128) of X_t. The head sums the KS partials in slice order and adds b1.
+// Lexp = T-1-t, the live-step count when no step was skipped: the parameter version to read is assumed from it so
+// the weight loads do not wait for cstate / msum; a skipped step (rare) re-issues them from the right buffer.
+__global__ __launch_bounds__(256) void coma_l1_kernel(CritArgs a, int t, int Lexp) {
+  const float mt = a.msum[t];
   const int L = a.cstate[0];
-  const bool pend = L > 0, owner = blockIdx.x == 0;
+  extern __shared__ float sm[];
+  constexpr int WP = KW + 1;
+  const int Kp = a.d.Kp, Kc = a.d.Kc, R = a.d.R;
+  const int ks = blockIdx.x, u0 = blockIdx.y * 16, rbase = blockIdx.z * kL1Rows;
+  const int k0 = ks * KW, kw = min(KW, Kp - k0), kwc = max(0, min(KW, Kc - k0));   // staged / real columns
+  const int nr = min(kL1Rows, R - rbase);
+  float* Ws = sm;               // [16][WP]
+  float* Xs = Ws + 16 * WP;     // [kL1Rows][WP]
+  __shared__ float sh[4];
+  const int tid = threadIdx.x;
+  const int owner = blockIdx.z == 0;
+  // W1 slice: 16 rows of kwc elements; all loads (params, grads, square_avg) in flight with X_t's
+  constexpr int NE = (16 * KW + 255) / 256;
+  auto widx = [&](int e) { const int u = e / KW, k = e - u * KW; return a.o_w1 + (int64_t)(u0 + u) * Kc + k0 + k; };
+  StageRegs<NE> wr;
+  auto load_w = [&](int from) {
+#pragma unroll
+    for (int q = 0; q < NE; ++q) {
+      const int e = tid + 256 * q, u = e / KW, k = e - u * KW;
+      const bool ok = e < 16 * KW && k < kwc;
+      const int64_t i = ok ? widx(e) : a.o_w1;
+      wr.p[q] = a.P[from][i];
+      wr.g[q] = a.G[i];
+      wr.s[q] = a.SQ[from][i];
+    }
+  };
+  const int src_spec = Lexp > 0 ? (Lexp - 1) & 1 : 0;
+  load_w(src_spec);
+  const int nv = kw / 4;   // b128 per row
+  constexpr int XB = (kL1Rows * KW / 4 + 255) / 256;
+  f32x4 xv[XB];
+#pragma unroll
+  for (int q = 0; q < XB; ++q) {
+    const int e = tid + 256 * q, rr = e / nv, kv = e - rr * nv;
+    xv[q] = (rr < nr) ? *(const f32x4*)&a.X[((int64_t)t * R + rbase + rr) * Kp + k0 + 4 * kv] : f32x4{0, 0, 0, 0};
+  }
+  if (!(mt > 0.0f)) return;   // step skipped (coma_learner.py:121-122)
+  const bool pend = L > 0;
   const int src = pend ? (L - 1) & 1 : 0, dst = L & 1;
+  if (src != src_spec) load_w(src);
   if (pend) crit_coef(a, sh);
   __syncthreads();
   const float inv = pend ? sh[0] : 0.0f, coef = pend ? sh[1] : 0.0f;
-  if (pend && owner && blockIdx.y == 0 && tid == 0) a.crec[a.cstate[1] * 8 + 5] = sh[2];
-  // W1 rows u0 .. u0+15 (contiguous in the reference layout: 16 * Kc elements), zero-padded to Kp in LDS
-  for (int e = tid; e < 16 * (Kp - Kc); e += 256) Ws[(e / (Kp - Kc)) * KP + Kc + e % (Kp - Kc)] = 0.0f;
-  crit_stage(a, 16 * Kc, pend, inv, coef, src, dst, owner,
-             [&](int e) { return a.o_w1 + (int64_t)u0 * Kc + e; },
-             [&](int e, float v) { const int u = e / Kc; Ws[u * KP + (e - u * Kc)] = v; });
-  crit_stage(a, 16, pend, inv, coef, src, dst, owner, [&](int e) { return a.o_b1 + u0 + e; },
-             [&](int e, float v) { bs[e] = v; });
-  if (pend) {   // fc2 / fc3 (contiguous [o_w2, Pc)): each l1 block updates one slice, head reads the result
-    const int nb = gridDim.x * gridDim.y, lb = blockIdx.y * gridDim.x + blockIdx.x;
-    const int64_t NT = a.Pc - a.o_w2, chunk = (NT + nb - 1) / nb, beg = lb * chunk;
-    const int cnt = (int)max<int64_t>(0, min<int64_t>(chunk, NT - beg));
-    crit_stage(a, cnt, true, inv, coef, src, dst, true, [&](int e) { return a.o_w2 + beg + e; },
-               [&](int, float) {});
-  }
-  {   // X_t rows r0 .. r0+15: b128 loads, all in flight before the LDS stores
-    const int nv = Kp / 4;
-    constexpr int XB = 8;
-    for (int e0 = tid; e0 < 16 * nv; e0 += 256 * XB) {
-      f32x4 xv[XB];
+  if (pend && owner && ks == 0 && blockIdx.y == 0 && tid == 0) a.crec[a.cstate[1] * 8 + 5] = sh[2];
 #pragma unroll
-      for (int u = 0; u < XB; ++u) {
-        const int e = min(e0 + 256 * u, 16 * nv - 1), rr = e / nv, kv = e - rr * nv;
-        xv[u] = r0 + rr < R ? *(const f32x4*)&a.X[((int64_t)t * R + r0 + rr) * Kp + 4 * kv] : f32x4{0, 0, 0, 0};
-      }
-#pragma unroll
-      for (int u = 0; u < XB; ++u) {
-        const int e = e0 + 256 * u;
-        if (e >= 16 * nv) break;
-        const int rr = e / nv, kv = e - rr * nv;
-        float* d = &Xs[rr * KP + 4 * kv];
-        d[0] = xv[u][0]; d[1] = xv[u][1]; d[2] = xv[u][2]; d[3] = xv[u][3];
+  for (int q = 0; q < NE; ++q) {
+    const int e = tid + 256 * q, u = e / KW, k = e - u * KW;
+    if (e >= 16 * KW) break;
+    float p = 0.0f;
+    if (k < kwc) {
+      p = wr.p[q];
+      if (pend) {
+        const float g = (wr.g[q] * inv) * coef;
+        const float v = wr.s[q] * a.hp.alpha + (1.0f - a.hp.alpha) * (g * g);
+        p = p + (-a.hp.lr) * (g / (sqrtf(v) + a.hp.eps));
+        if (owner) {
+          const int64_t i = widx(e);
+          a.SQ[dst][i] = v;
+          a.P[dst][i] = p;
+        }
       }
     }
+    Ws[u * WP + k] = p;
+  }
+#pragma unroll
+  for (int q = 0; q < XB; ++q) {
+    const int e = tid + 256 * q, rr = e / nv, kv = e - rr * nv;
+    if (rr >= kL1Rows) break;
+    float* d = &Xs[rr * WP + 4 * kv];
+    d[0] = xv[q][0]; d[1] = xv[q][1]; d[2] = xv[q][2]; d[3] = xv[q][3];
+  }
+  if (pend && ks == 0 && owner) {   // fc1.bias and fc2 / fc3: one slice per (ut) block of the first K slice
+    const int nb = gridDim.y, lb = blockIdx.y;
+    const int64_t beg0 = a.o_b1, NT = a.Pc - a.o_b1;   // fc1.bias, fc2.*, fc3.* are contiguous from o_b1
+    const int64_t chunk = (NT + nb - 1) / nb, beg = beg0 + lb * chunk;
+    const int cnt = (int)max<int64_t>(0, min<int64_t>(chunk, a.Pc - beg));
+    crit_stage(a, cnt, true, inv, coef, src, dst, true, [&](int e) { return beg + e; }, [&](int, float) {});
   }
   __syncthreads();
   const int w = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
-  const int Kq = (Kp + 15) / 16 * 4;
-  const int kb = w * Kq, ke = min(Kp, kb + Kq);
-  f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
-  int k = kb;
-  for (; k + 8 <= ke; k += 8) {
-    acc0 = mfma_f32_16x4(Xs[c * KP + k + g], Ws[c * KP + k + g], acc0);
-    acc1 = mfma_f32_16x4(Xs[c * KP + k + 4 + g], Ws[c * KP + k + 4 + g], acc1);
-  }
-  if (k < ke) acc0 = mfma_f32_16x4(Xs[c * KP + k + g], Ws[c * KP + k + g], acc0);
+  for (int rt = w; rt * 16 < nr; rt += 4) {   // row tiles of 16 over the waves, the whole K slice each
+    f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+    const float* xr = Xs + (16 * rt + c) * WP + g;
+    const float* wrow = Ws + c * WP + g;
+    int k = 0;
+    for (; k + 8 <= kw; k += 8) {
+      acc0 = mfma_f32_16x4(xr[k], wrow[k], acc0);
+      acc1 = mfma_f32_16x4(xr[k + 4], wrow[k + 4], acc1);
+    }
+    if (k < kw) acc0 = mfma_f32_16x4(xr[k], wrow[k], acc0);
+    float* out = a.H1p + ((int64_t)ks * R + rbase + 16 * rt) * CH + u0 + c;
 #pragma unroll
-  for (int reg = 0; reg < 4; ++reg) red[(w * 16 + 4 * g + reg) * 16 + c] = acc0[reg] + acc1[reg];
-  __syncthreads();
-  {
-    const int i = tid >> 4, j = tid & 15;
-    const float v = ((red[(0 * 16 + i) * 16 + j] + red[(1 * 16 + i) * 16 + j]) +
-                     (red[(2 * 16 + i) * 16 + j] + red[(3 * 16 + i) * 16 + j])) + bs[j];
-    if (r0 + i < R) a.H1c[(int64_t)(r0 + i) * CH + u0 + j] = fmaxf(v, 0.0f);
+    for (int reg = 0; reg < 4; ++reg)
+      if (16 * rt + 4 * g + reg < nr) out[(int64_t)(4 * g + reg) * CH] = acc0[reg] + acc1[reg];
   }
 }
 
 // head: for a 16-row tile, H2 = relu(H1 W2^T + b2), Q = H2 W3^T + b3, the TD error against the TD(lambda) target,
 // the loss sums, dQ (unnormalised: d sum (td m)^2 / dq_taken = 2 td m m), dH2 = dQ W3 o [H2 > 0], dH1 = dH2 W2 o
 // [H1 > 0]. Stages (and applies the pending update to) W2 / b2 / W3 / b3; block 0 writes them back.
-__global__ __launch_bounds__(256) void coma_head_kernel(CritArgs a, int t) {
-  if (!(a.msum[t] > 0.0f)) return;
+__global__ __launch_bounds__(kHeadThreads) void coma_head_kernel(CritArgs a, int t, int Lexp) {
+  const float mt = a.msum[t];
+  const int L = a.cstate[0];
   extern __shared__ float sm[];
   constexpr int CP = CH + 1;
   const int A = a.d.A, A16 = (A + 15) / 16 * 16, R = a.d.R, n = a.d.n;
@@ -351,52 +448,56 @@ __global__ __launch_bounds__(256) void coma_head_kernel(CritArgs a, int t) {
   __shared__ int acts[16];
   __shared__ float part[16][5];
   const int tid = threadIdx.x, r0 = blockIdx.x * 16;
-  // fc2 / fc3 at this step's version (l1 applied the pending update into P[L & 1])
-  const float* Pv = a.P[a.cstate[0] & 1];
-  {
+  // fc2 / fc3 at this step's version (l1 applied the pending update into P[L & 1]), assumed from Lexp
+  const float* Pv = a.P[Lexp & 1];
+  auto load_fc = [&]() {
     constexpr int NB = 16;
     const int N2 = CH * CH / 4, N3 = A * CH / 4;   // b128 units (CH = 128: rows never straddle a unit)
-    for (int e0 = tid; e0 < N2 + N3; e0 += 256 * NB) {
+    for (int e0 = tid; e0 < N2 + N3; e0 += kHeadThreads * NB) {
       f32x4 v[NB];
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
-        const int e = min(e0 + 256 * u, N2 + N3 - 1);
+        const int e = min(e0 + kHeadThreads * u, N2 + N3 - 1);
         v[u] = e < N2 ? *(const f32x4*)&Pv[a.o_w2 + 4 * e] : *(const f32x4*)&Pv[a.o_w3 + 4 * (e - N2)];
       }
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
-        const int e = e0 + 256 * u;
+        const int e = e0 + kHeadThreads * u;
         if (e >= N2 + N3) break;
         float* d = e < N2 ? &W2s[((4 * e) >> 7) * CP + ((4 * e) & 127)]
                           : &W3s[((4 * (e - N2)) >> 7) * CP + ((4 * (e - N2)) & 127)];
         d[0] = v[u][0]; d[1] = v[u][1]; d[2] = v[u][2]; d[3] = v[u][3];
       }
     }
+  };
+  load_fc();
+  if (!(mt > 0.0f)) return;
+  if ((L & 1) != (Lexp & 1)) {   // a skipped step shifted the version parity
+    Pv = a.P[L & 1];
+    load_fc();
   }
-  for (int e = A * CH + tid; e < A16 * CH; e += 256) W3s[(e >> 7) * CP + (e & 127)] = 0.0f;
+  for (int e = A * CH + tid; e < A16 * CH; e += kHeadThreads) W3s[(e >> 7) * CP + (e & 127)] = 0.0f;
   if (tid < CH) b2s[tid] = Pv[a.o_b2 + tid];
   if (tid < A) b3s[tid] = Pv[a.o_b3 + tid];
   if (tid >= A && tid < A16) b3s[tid] = 0.0f;
-  {
-    f32x4 hv[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + 256 * u, i = e >> 5, kv = e & 31;
-      hv[u] = r0 + i < R ? *(const f32x4*)&a.H1c[(int64_t)(r0 + i) * CH + 4 * kv] : f32x4{0, 0, 0, 0};
+  if (tid < 512) {   // H1 = relu(sum of the K-slice partials in slice order + b1): 16 x 128 = 512 b128
+    const int i = tid >> 5, kv = tid & 31;
+    f32x4 hv = {0, 0, 0, 0};
+    if (r0 + i < R) {
+      for (int ks = 0; ks < a.KS; ++ks) hv += *(const f32x4*)&a.H1p[((int64_t)ks * R + r0 + i) * CH + 4 * kv];
+      const f32x4 bb = *(const f32x4*)&Pv[a.o_b1 + 4 * kv];
+      hv += bb;
+      hv[0] = fmaxf(hv[0], 0.0f); hv[1] = fmaxf(hv[1], 0.0f); hv[2] = fmaxf(hv[2], 0.0f); hv[3] = fmaxf(hv[3], 0.0f);
+      *(f32x4*)&a.H1c[(int64_t)(r0 + i) * CH + 4 * kv] = hv;
     }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = tid + 256 * u, i = e >> 5, kv = e & 31;
-      float* d = &H1s[i * CP + 4 * kv];
-      d[0] = hv[u][0]; d[1] = hv[u][1]; d[2] = hv[u][2]; d[3] = hv[u][3];
-    }
+    float* d = &H1s[i * CP + 4 * kv];
+    d[0] = hv[0]; d[1] = hv[1]; d[2] = hv[2]; d[3] = hv[3];
   }
   __syncthreads();
   const int w = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
-  // H2 = relu(H1 W2^T + b2): wave w owns unit tiles w and w + 4
-#pragma unroll
-  for (int jj = 0; jj < 2; ++jj) {
-    const int jt = w + 4 * jj;
+  // H2 = relu(H1 W2^T + b2): wave w < 8 owns unit tile w
+  if (w < 8) {
+    const int jt = w;
     f32x4 acc = {0, 0, 0, 0};
     for (int k = 0; k < CH; k += 4) acc = mfma_f32_16x4(H1s[c * CP + k + g], W2s[(16 * jt + c) * CP + k + g], acc);
 #pragma unroll
@@ -405,7 +506,7 @@ __global__ __launch_bounds__(256) void coma_head_kernel(CritArgs a, int t) {
   }
   __syncthreads();
   // Q = H2 W3^T + b3
-  for (int qt = w; qt < A16 / 16; qt += 4) {
+  for (int qt = w; qt < A16 / 16; qt += kHeadThreads / 64) {
     f32x4 acc = {0, 0, 0, 0};
     for (int k = 0; k < CH; k += 4) acc = mfma_f32_16x4(H2s[c * CP + k + g], W3s[(16 * qt + c) * CP + k + g], acc);
 #pragma unroll
@@ -436,7 +537,7 @@ __global__ __launch_bounds__(256) void coma_head_kernel(CritArgs a, int t) {
     dqs[tid] = dq;
     acts[tid] = at;
   }
-  for (int e = tid; e < 16 * A; e += 256) {   // the Q values the actor's baseline uses (coma_learner.py:126)
+  for (int e = tid; e < 16 * A; e += kHeadThreads) {   // the Q values the actor's baseline uses (coma_learner.py:126)
     const int i = e / A, aa = e - i * A;
     if (r0 + i < R) a.qvals[((int64_t)t * R + r0 + i) * A + aa] = Qs[i * (A16 + 1) + aa];
   }
@@ -447,7 +548,7 @@ __global__ __launch_bounds__(256) void coma_head_kernel(CritArgs a, int t) {
     a.cpart[blockIdx.x * 8 + tid] = s;
   }
   // dH2 = dQ W3 o [H2 > 0] (dQ is one-hot at the taken action)
-  for (int e = tid; e < 16 * CH; e += 256) {
+  for (int e = tid; e < 16 * CH; e += kHeadThreads) {
     const int i = e >> 7, u = e & 127;
     const float h2 = H2s[i * CP + u];
     const float v = h2 > 0.0f ? dqs[i] * W3s[acts[i] * CP + u] : 0.0f;
@@ -459,9 +560,8 @@ __global__ __launch_bounds__(256) void coma_head_kernel(CritArgs a, int t) {
   }
   __syncthreads();
   // dH1 = dH2 W2 o [H1 > 0]: B[kk][j] = W2[kk][j]
-#pragma unroll
-  for (int jj = 0; jj < 2; ++jj) {
-    const int jt = w + 4 * jj;
+  if (w < 8) {
+    const int jt = w;
     f32x4 acc = {0, 0, 0, 0};
     for (int k = 0; k < CH; k += 4) acc = mfma_f32_16x4(dHs[c * CP + k + g], W2s[(k + g) * CP + 16 * jt + c], acc);
 #pragma unroll
@@ -486,7 +586,7 @@ __host__ __device__ inline int wgrad_blocks(const CDims& d) {
 }
 
 __global__ __launch_bounds__(256) void coma_wgrad_kernel(CritArgs a, int t) {
-  if (!(a.msum[t] > 0.0f)) return;
+  const float mt = a.msum[t];   // checked once the first operands are in flight
   const int R = a.d.R, Kp = a.d.Kp, Kc = a.d.Kc, A = a.d.A;
   const int N1 = (Kc + 1 + 63) / 64, A16 = (A + 15) / 16 * 16;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
@@ -516,13 +616,18 @@ __global__ __launch_bounds__(256) void coma_wgrad_kernel(CritArgs a, int t) {
       if (rr >= R) return 0.0f;
       return jc < ncol ? Bop[(int64_t)rr * ldb + jc] : (jc == ncol ? 1.0f : 0.0f);
     };
-    int r = 0;
-    for (; r + 8 <= R; r += 8) {
-      const float a0 = opA(r + g), b0 = opB(r + g), a1 = opA(r + 4 + g), b1 = opB(r + 4 + g);
-      acc0 = mfma_f32_16x4(a0, b0, acc0);
-      acc1 = mfma_f32_16x4(a1, b1, acc1);
+    constexpr int RC = 32;   // k-steps of 4 rows whose operands are loaded in one round trip
+    for (int r0 = 0; r0 < R; r0 += 4 * RC) {
+      float av[RC], bv[RC];
+#pragma unroll
+      for (int q = 0; q < RC; ++q) { av[q] = opA(r0 + 4 * q + g); bv[q] = opB(r0 + 4 * q + g); }
+      if (r0 == 0 && !(mt > 0.0f)) return;
+#pragma unroll
+      for (int q = 0; q < RC; q += 2) {
+        acc0 = mfma_f32_16x4(av[q], bv[q], acc0);
+        acc1 = mfma_f32_16x4(av[q + 1], bv[q + 1], acc1);
+      }
     }
-    for (; r < R; r += 4) acc0 = mfma_f32_16x4(opA(r + g), opB(r + g), acc0);
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
       const int row = u0 + 4 * g + reg;
@@ -533,6 +638,8 @@ __global__ __launch_bounds__(256) void coma_wgrad_kernel(CritArgs a, int t) {
         sq = fmaf(v, v, sq);
       }
     }
+  } else if (!(mt > 0.0f)) {
+    return;
   } else if (tid == 0) {
     float* rec = a.crec + t * 8;
     for (int k = 0; k < 5; ++k) {

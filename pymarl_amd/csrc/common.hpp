@@ -12,7 +12,11 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 namespace mq {
 
 // Two f32 FMAs in one v_pk_fma_f32 (half the issue slots of two v_fma_f32 at the same FLOP rate).
+#ifdef MQ_SCALAR_FMA
+MQ_DEV f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return f32x2{fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y)}; }
+#else
 MQ_DEV f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+#endif
 
 constexpr float kNegMask = -9999999.0f;   // q_learner.py:68,74
 
