@@ -96,6 +96,8 @@ class EpisodeBatch:
             else:
                 raise KeyError("{} not found in transition or episode data".format(k))
             dtype = self.scheme[k].get("dtype", th.float32)
+            if not th.is_tensor(v):
+                v = np.asarray(v)   # one host array, one host-to-device copy per field
             v = th.as_tensor(v, dtype=dtype, device=self.device)
             dest = target[k][_slices]
             self._check_safe_view(v, dest)
