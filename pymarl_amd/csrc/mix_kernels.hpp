@@ -214,3 +214,212 @@ __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* _
 }
 
 }  // namespace mq
+
+namespace mq {
+
+// mix_kernel with every independent load of a wave issued up front (A <= MA actions, n <= MN agents, E <= 64):
+// the agent's Q rows at t+1 (both nets), its avail row and action, the QMIX hypernet outputs of both nets, V.2 and
+// the mask / reward / terminated words, all in one round trip; only the chosen-action value waits on the action.
+// The generic kernel fetches them in dependent stages (action -> chosen, argmax blocks -> target value, then the
+// hypernet rows after a barrier). Same arithmetic in the same order: bitwise-identical outputs.
+template <int MA, int MN>
+__global__ __launch_bounds__(256) void mix_fast_kernel(Dims d, Rep rp, const float* __restrict__ P0,
+                                                       const float* __restrict__ P1, Lay L, Work w,
+                                                       int32_t* curmax_out) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + wv;
+  const int n = d.n, A = d.A, E = d.E, R = d.R, NH = d.NH;
+  const bool qmix = d.mixer == MQ_MIXER_QMIX;
+  __shared__ float chs[4][64], tms[4][64], dps[4][64];
+  __shared__ float w1s[4][MN][65];   // |hyper_w_1| rows of the online mixer, for dLoss/dchosen
+  __shared__ float red[4][8];
+  __shared__ float v2red[4][65];
+  float l2 = 0.0f, msk = 0.0f, abs_ = 0.0f, qs = 0.0f, tg = 0.0f;
+  float dv2 = 0.0f, dv2b = 0.0f;
+  const bool valid = m < d.M;
+  int t = 0, b = 0;
+  int64_t ep = 0;
+  if (valid) {
+    t = (int)fdiv((uint32_t)m, d.dB);
+    b = m - t * d.B;
+    ep = rp.ep(b);
+  }
+  const int64_t slot = ep * d.t_stride + t;
+  const float* Qon = w.Q;
+  const float* Qtg = w.Q + d.RT() * A;
+  // ---- every independent load of the wave
+  const bool agent_lane = valid && lane < n;
+  const int r = b * n + min(lane, n - 1);
+  int at = 0;
+  float qsel[MA], qtr[MA];
+  int32_t avr[MA];
+  if (agent_lane) {
+    at = (int)rp.actions[slot * n + lane];
+    const float* qn = Qon + ((int64_t)(t + 1) * R + r) * A;
+    const float* qt = Qtg + ((int64_t)(t + 1) * R + r) * A;
+    const float* qs_row = d.double_q ? qn : qt;
+    const int32_t* av = rp.avail + ((slot + 1) * n + lane) * (int64_t)A;
+#pragma unroll
+    for (int u = 0; u < MA; ++u) {
+      const int a = min(u, A - 1);
+      qsel[u] = qs_row[a];
+      qtr[u] = qt[a];
+      avr[u] = av[a];
+    }
+  }
+  const bool e_lane = qmix && valid && lane < E;
+  float won[MN], wtg[MN], xon[3], xtg[3], v2w0 = 0.0f, v2w1 = 0.0f;
+  if (e_lane) {
+    const float* hon = w.HYP + (int64_t)m * NH;
+    const float* htg = w.HYP + ((int64_t)d.M + m) * NH;
+#pragma unroll
+    for (int ag = 0; ag < MN; ++ag) {
+      won[ag] = hon[min(ag, n - 1) * E + lane];
+      wtg[ag] = htg[min(ag, n - 1) * E + lane];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {   // hyper_w_final, hyper_b_1, V.0 outputs
+      xon[k] = hon[n * E + k * E + lane];
+      xtg[k] = htg[n * E + k * E + lane];
+    }
+    v2w0 = P0[L.o[MQ_P_V2_W] + lane];
+    v2w1 = P1[L.o[MQ_P_V2_W] + lane];
+  }
+  float mask = 0.0f, rew = 0.0f, term = 0.0f;
+  if (valid) {
+    mask = (float)rp.filled[slot];
+    if (t > 0) mask *= 1.0f - (float)rp.term[slot - 1];   // q_learner.py:42-43
+    rew = rp.reward[slot];
+    term = (float)rp.term[slot];
+  }
+  const float v2b0 = qmix ? P0[L.o[MQ_P_V2_B]] : 0.0f, v2b1 = qmix ? P1[L.o[MQ_P_V2_B]] : 0.0f;
+  // ---- chosen value and double-Q selection (q_learner.py:55, 68-78), first index on ties
+  float chosen = 0.0f, tmax = 0.0f;
+  if (agent_lane) {
+    chosen = Qon[((int64_t)t * R + r) * A + at];
+    float best = 0.0f;
+    int cur = 0;
+#pragma unroll
+    for (int u = 0; u < MA; ++u) {
+      const float v = avr[u] ? qsel[u] : kNegMask;
+      if (u < A && (u == 0 || v > best)) { best = v; cur = u; }
+    }
+    if (d.double_q) {
+      float qc = 0.0f;
+      int ac = 0;
+#pragma unroll
+      for (int u = 0; u < MA; ++u)
+        if (u == cur) { qc = qtr[u]; ac = avr[u]; }
+      tmax = ac ? qc : kNegMask;
+    } else {
+      tmax = best;
+    }
+    if (curmax_out) curmax_out[(int64_t)t * R + r] = cur;
+  }
+  chs[wv][lane] = chosen;
+  tms[wv][lane] = tmax;
+  if (e_lane) {
+#pragma unroll
+    for (int ag = 0; ag < MN; ++ag) w1s[wv][ag][lane] = fabsf(won[ag]);
+  }
+  __syncthreads();
+  const float gamma = d.gamma;
+  if (qmix) {
+    // QMIX forward of both nets (qmix_fwd_lane's arithmetic, operands from registers)
+    float y = 0.0f, yt = 0.0f, pre = 0.0f, hid = 0.0f;
+    {
+      float prod = 0.0f, vt = 0.0f, prod_t = 0.0f, vt_t = 0.0f;
+      if (e_lane) {
+        float acc = 0.0f, acc_t = 0.0f;
+#pragma unroll
+        for (int ag = 0; ag < MN; ++ag) {
+          if (ag < n) {
+            acc = fmaf(chs[wv][ag], fabsf(won[ag]), acc);
+            acc_t = fmaf(tms[wv][ag], fabsf(wtg[ag]), acc_t);
+          }
+        }
+        pre = acc + xon[1];
+        hid = eluf(pre);
+        prod = hid * fabsf(xon[0]);
+        vt = fmaxf(xon[2], 0.0f) * v2w0;
+        const float pre_t = acc_t + xtg[1];
+        prod_t = eluf(pre_t) * fabsf(xtg[0]);
+        vt_t = fmaxf(xtg[2], 0.0f) * v2w1;
+      }
+      y = wave_sum(prod) + (wave_sum(vt) + v2b0);
+      yt = wave_sum(prod_t) + (wave_sum(vt_t) + v2b1);
+    }
+    if (!valid) y = yt = 0.0f;
+    const float target = rew + gamma * (1.0f - term) * yt;   // q_learner.py:86
+    const float td = y - target;
+    const float mtd = td * mask;
+    l2 = mtd * mtd; msk = mask; abs_ = fabsf(mtd); qs = y * mask; tg = target * mask;
+    const float dy = (2.0f * mtd) * mask;
+    float dpre = 0.0f;
+    if (e_lane) {
+      const float wf = fabsf(xon[0]);
+      const float dhid = dy * wf;
+      float* dh = w.dHYP + (int64_t)m * NH;
+      dh[n * E + lane] = dy * hid * sgnf(xon[0]);                             // hyper_w_final
+      dpre = dhid * (pre > 0.0f ? 1.0f : expf(pre));                          // elu'
+      dh[n * E + E + lane] = dpre;                                            // hyper_b_1
+      dh[n * E + 2 * E + lane] = dy * v2w0 * (xon[2] > 0.0f ? 1.0f : 0.0f);   // V.0 (through relu)
+      dv2 = dy * fmaxf(xon[2], 0.0f);                                         // V.2 weight
+#pragma unroll
+      for (int ag = 0; ag < MN; ++ag)                                         // hyper_w_1 (through |.|)
+        if (ag < n) dh[ag * E + lane] = (chs[wv][ag] * dpre) * sgnf(won[ag]);
+    }
+    dv2b = dy;
+    dps[wv][lane] = dpre;
+    __syncthreads();
+    if (agent_lane) {
+      float acc = 0.0f;
+      for (int e = 0; e < E; ++e) acc = fmaf(w1s[wv][lane][e], dps[wv][e], acc);
+      w.dch[(int64_t)t * R + b * n + lane] = acc;
+    }
+  } else {
+    float y, yt;
+    if (d.mixer == MQ_MIXER_VDN) {
+      y = wave_sum(lane < n ? chosen : 0.0f);
+      yt = wave_sum(lane < n ? tmax : 0.0f);
+    } else {
+      y = chosen;
+      yt = tmax;
+    }
+    const float target = rew + gamma * (1.0f - term) * yt;
+    const float td = y - target;
+    const float mtd = td * mask;
+    const float dy = (2.0f * mtd) * mask;
+    if (d.mixer == MQ_MIXER_VDN) {
+      l2 = mtd * mtd; msk = mask; abs_ = fabsf(mtd); qs = y * mask; tg = target * mask;
+    } else {
+      const bool on = lane < n;
+      l2 = wave_sum(on ? mtd * mtd : 0.0f);
+      msk = wave_sum(on ? mask : 0.0f);
+      abs_ = wave_sum(on ? fabsf(mtd) : 0.0f);
+      qs = wave_sum(on ? y * mask : 0.0f);
+      tg = wave_sum(on ? target * mask : 0.0f);
+    }
+    if (agent_lane) w.dch[(int64_t)t * R + b * n + lane] = dy;
+    __syncthreads();
+  }
+  if (!valid) { l2 = msk = abs_ = qs = tg = 0.0f; dv2 = dv2b = 0.0f; }
+  if (lane == 0) {
+    red[wv][0] = l2; red[wv][1] = msk; red[wv][2] = abs_; red[wv][3] = qs; red[wv][4] = tg;
+    v2red[wv][64] = dv2b;
+  }
+  v2red[wv][lane] = dv2;
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    const int c = threadIdx.x;
+    float* out = w.loss_part + (int64_t)blockIdx.x * 8;
+    out[c] = c < 5 ? ((red[0][c] + red[1][c]) + (red[2][c] + red[3][c])) : 0.0f;
+  }
+  if (qmix && threadIdx.x <= E) {
+    const int e = threadIdx.x == E ? 64 : threadIdx.x;
+    w.slab_v2[(int64_t)blockIdx.x * (E + 1) + threadIdx.x] =
+        (v2red[0][e] + v2red[1][e]) + (v2red[2][e] + v2red[3][e]);
+  }
+}
+
+}  // namespace mq

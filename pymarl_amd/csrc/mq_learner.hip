@@ -85,7 +85,8 @@ struct mq_handle {
   bool force_unfused = getenv("MQ_UNFUSED_FWD") != nullptr;       // A/B switch for the fused agent forward
   bool force_unfused_bwd = getenv("MQ_UNFUSED_BWD") != nullptr;   // A/B switch for the fused BPTT
   bool force_unfused_mix = getenv("MQ_GEMM_HYPER") != nullptr;   // A/B switch: hypernet through gemm_f32
-  int dwh_split = getenv("MQ_DWH_SPLIT") ? atoi(getenv("MQ_DWH_SPLIT")) : 8;   // m-slices of the dW_hyper pass
+  int dwh_split = getenv("MQ_DWH_SPLIT") ? atoi(getenv("MQ_DWH_SPLIT")) : 16;  // m-slices of the dW_hyper pass
+  bool generic_mix = getenv("MQ_GENERIC_MIX") != nullptr;   // A/B switch: mix_kernel instead of mix_fast_kernel
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
   int slots = 0;
@@ -416,9 +417,19 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   }
   pt.begin(PH_MIX);
   h->nblk_mix = (d.M + 3) / 4;
-  hipLaunchKernelGGL(mix_kernel, dim3(h->nblk_mix), dim3(256), 0, s, d, rp, (const float*)h->on,
-                     (const float*)h->tg, L, w, curmax);
-  MQ_HIP(hipGetLastError());
+  {
+    const bool fast = d.n <= 16 && d.E <= 64 && !h->generic_mix;
+    if (fast && d.A <= 16)
+      hipLaunchKernelGGL((mix_fast_kernel<16, 16>), dim3(h->nblk_mix), dim3(256), 0, s, d, rp, (const float*)h->on,
+                         (const float*)h->tg, L, w, curmax);
+    else if (fast && d.A <= 32)
+      hipLaunchKernelGGL((mix_fast_kernel<32, 16>), dim3(h->nblk_mix), dim3(256), 0, s, d, rp, (const float*)h->on,
+                         (const float*)h->tg, L, w, curmax);
+    else
+      hipLaunchKernelGGL(mix_kernel, dim3(h->nblk_mix), dim3(256), 0, s, d, rp, (const float*)h->on,
+                         (const float*)h->tg, L, w, curmax);
+    MQ_HIP(hipGetLastError());
+  }
   pt.begin(PH_GRUB);
   const int rw_bwd = std::min(2, pick_rw(d.R, 256));
   if (rw_bwd == 1 && fused_bwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused_bwd) {

@@ -206,3 +206,25 @@ def test_data_parallel_norm_path_single_rank(cases):
         outs.append((flat_params(learner), learner.last_stats()["grad_norm"]))
     assert rel(outs[1][0], outs[0][0]) < 1e-6
     assert abs(outs[1][1] - outs[0][1]) <= 1e-5 * abs(outs[0][1])
+
+
+@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_vdn", "tiny_qmix"])
+def test_fast_mix_kernel_bitwise(cases, name, monkeypatch):
+    """mix_fast_kernel (every load issued up front) equals the generic mix_kernel bit for bit."""
+    from tests.gpu_helpers import build, flat_params
+    case = get_case(cases, name)
+    outs = []
+    for generic in (False, True):
+        if generic:
+            monkeypatch.setenv("MQ_GENERIC_MIX", "1")
+        else:
+            monkeypatch.delenv("MQ_GENERIC_MIX", raising=False)
+        args, buf, mac, learner, logger = build(case)
+        np.random.seed(case.sampler_seed)
+        for k in range(2):
+            batch = buf.sample(case.B)
+            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
+        outs.append((flat_params(learner), learner.last_stats(), learner.last_cur_max_actions().cpu().numpy()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert outs[0][1] == outs[1][1]
+    assert np.array_equal(outs[0][2], outs[1][2])
