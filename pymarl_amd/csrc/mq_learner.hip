@@ -85,7 +85,7 @@ struct mq_handle {
   bool force_unfused = getenv("MQ_UNFUSED_FWD") != nullptr;       // A/B switch for the fused agent forward
   bool force_unfused_bwd = getenv("MQ_UNFUSED_BWD") != nullptr;   // A/B switch for the fused BPTT
   bool force_unfused_mix = getenv("MQ_GEMM_HYPER") != nullptr;   // A/B switch: hypernet through gemm_f32
-  int dwh_split = getenv("MQ_DWH_SPLIT") ? atoi(getenv("MQ_DWH_SPLIT")) : 16;  // m-slices of the dW_hyper pass
+  int dwh_split = getenv("MQ_DWH_SPLIT") ? atoi(getenv("MQ_DWH_SPLIT")) : 8;   // m-slices of the dW_hyper pass
   bool generic_mix = getenv("MQ_GENERIC_MIX") != nullptr;   // A/B switch: mix_kernel instead of mix_fast_kernel
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded

@@ -13,7 +13,8 @@ import sys
 from collections import defaultdict
 
 PHASES = {"Fc1Prob": "fc1", "GiProb": "gi", "gru_fwd": "gru_fwd", "Fc2Prob": "fc2", "HypProb": "hyper",
-          "mix_kernel": "mix", "gru_bwd": "gru_bwd", "Dx1Prob": "dx1", "Dw1Prob": "dw1", "DwhProb": "dwh",
+          "hyper_ws_kernel": "hyper", "hyper_kernel": "hyper", "mix_kernel": "mix", "mix_fast_kernel": "mix",
+          "gru_bwd": "gru_bwd", "Dx1Prob": "dx1", "Dw1Prob": "dw1", "DwhProb": "dwh", "dwh_kernel": "dwh",
           "red_pass": "reduce", "apply_kernel": "apply"}
 
 
