@@ -113,6 +113,7 @@ def build_workload(cfg_name, device, n_episodes=5000, unique=512, seed=0):
             buf.data.transition_data[k][start:start + m] = th.as_tensor(v[:m], device=device)
     buf.episode_lengths[:] = buf.data.transition_data["filled"].sum(1).reshape(-1).cpu().numpy()
     buf.episodes_in_buffer = n_episodes
+    th.manual_seed(seed)   # identical random-init weights on every rank (data-parallel replicas start equal)
     mac = mac_REGISTRY["basic_mac"](buf.scheme, groups, args)
     learner = le_REGISTRY["q_learner"](mac, buf.scheme, Logger(logging.getLogger("bench")), args)
     learner.cuda()
@@ -318,11 +319,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # MQ_BENCH_BACKEND=gloo + more ranks than GPUs: rehearsal of the N>1 control flow on a 1-GPU box (ranks share
+    # devices round-robin; RCCL refuses two ranks on one GPU). The driver's N>1 runs use the default, RCCL.
+    backend = os.environ.get("MQ_BENCH_BACKEND", "nccl")
+    dev_index = local_rank % max(1, th.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        th.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=th.device("cuda", local_rank))
-    device = th.device("cuda", local_rank)
+        th.cuda.set_device(dev_index)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=th.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
+    device = th.device("cuda", dev_index)
     th.cuda.set_device(device)
 
     args, buf, learner, data = build_workload(a.config, device)
