@@ -4,14 +4,16 @@
 // Critic (coma.py:22-58, fc 868 -> 128 -> 128 -> A at MMM2). Each train() takes one optimiser step per t in
 // reversed order, every step on B*n rows only, so the critic is a chain of T tiny dependent steps. One step is three
 // launches, split where the data dependence forces a grid-wide exchange:
-//   l1     H1 = relu(X_t W1^T + b1)                 grid (row tiles of 16) x (8 unit tiles of 16)
-//   head   H2, Q, TD error, loss sums, dQ, dH2, dH1 grid (row tiles of 16): rows are independent up to dH1
+//   l1     partial H1 pre-activations X_t W1^T over K slices     grid (K slices) x (8 unit tiles of 16) x (row tiles)
+//   head   sum of the partials + b1, relu, H2, Q, TD error, loss sums, dQ, dH2, dH1   (1024 threads)
 //   wgrad  dW1 = dH1^T X_t, dW2 = dH2^T H1, dW3, biases, per-workgroup sums of squares (each gradient element has
 //          exactly one writer: no slabs, no atomics)
-// The RMSprop update of step t+1 (clip coefficient from wgrad's sums of squares) is applied by the NEXT step's l1
-// (its W1 / b1 tile) and head (W2, b2, W3, b3) right where they stage the weights, so applying costs no launch;
-// the last step's update is one more launch after the loop. Every workgroup that stages a tile applies the update
-// to it in LDS; one designated workgroup writes params / square_avg / clipped grads back.
+// The RMSprop update of step t+1 (clip coefficient from wgrad's sums of squares) is applied inside step t's l1 while
+// it stages the weights, so applying costs no launch: every W1 slice is owned by exactly one l1 block (K-split),
+// which updates it in registers, writes the new version back and multiplies with it; the first K slice's blocks
+// update fc1.bias / fc2 / fc3 in slices, which head then reads. Versions ping-pong between the caller's buffers and
+// a shadow (live step L reads version L-1 from buffer (L-1)&1, writes version L to L&1), so no block reads what
+// another block of the same launch writes. The last step's update is one more launch after the loop.
 // Steps whose mask is empty are skipped on the device (coma_learner.py:121-122) and leave the pending update for the
 // next live step.
 //
