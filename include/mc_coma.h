@@ -12,6 +12,7 @@
  *   mc_update_targets  COMALearner._update_targets                       src/learners/coma_learner.py:150-152
  *   mc_policy          BasicMAC.forward pi_logits post-processing        src/controllers/basic_controller.py:53-73
  *   mc_copy_intermediate  (test hook) the critic's per-step Q values, the TD(lambda) targets, the policy
+ *   mc_set_data_parallel  no reference counterpart: data-parallel COMA ("COMA caveat")
  */
 #ifndef MC_COMA_H
 #define MC_COMA_H
@@ -65,6 +66,21 @@ int mc_policy(float* logits, const int32_t* avail, int32_t rows, int32_t n_actio
  * mc_phase_times writes the last step's [prologue, critic chain, actor] ms (synchronises on the events). */
 int mc_set_timing(mc_handle* h, int32_t on);
 int mc_phase_times(mc_handle* h, float* ms /* [3] */);
+/* Data-parallel COMA: each rank passes its contiguous shard of the same global sample to
+ * mc_train_step; the library calls `allreduce` at every exchange step, in stream order on `stream`:
+ *   once       the per-step mask sums (T floats, through `scratch`), so every rank skips the same steps
+ *              (coma_learner.py:121-122) and normalises by the global sum(mask);
+ *   per live critic step  the unnormalised critic gradient [Pc] (then its norm is recomputed from the sum);
+ *   once       the per-step critic stat sums (8*T floats, through `scratch`; rank != 0 contributes zeros for the
+ *              replicated fields);
+ *   once       the agent gradient + sums [Pa + MQ_NSUMS] (then its norm is recomputed).
+ * `allreduce(buf, count, stream, ctx)` sums `count` floats at the device pointer `buf` over the ranks in place and
+ * returns 0 on success; `buf` is always critic_grad, agent_grad or `scratch` (all caller-owned). In this mode the
+ * host reads the global mask sums back once per train (one synchronisation) to know the live steps.
+ * `scratch` holds >= 8 * max_seq floats. allreduce = NULL switches data parallelism off. */
+typedef int (*mc_allreduce_fn)(float* buf, int64_t count, void* stream, void* ctx);
+int mc_set_data_parallel(mc_handle* h, mc_allreduce_fn allreduce, void* ctx, int32_t rank, float* scratch,
+                         int64_t scratch_count);
 /* 0 = critic Q values the actor used [T][B*n][A]; 1 = TD(lambda) targets [T][B*n]; 2 = policy pi [T][B*n][A]. */
 int mc_copy_intermediate(mc_handle* h, int which, float* dst, int64_t* count, void* stream);
 

@@ -28,8 +28,11 @@ EXPORTS = [
     "mq_greedy_actions", "mq_set_timing", "mq_phase_times", "mq_phase_names", "mq_set_data_parallel",
     # include/mc_coma.h
     "mc_create", "mc_destroy", "mc_param_offsets", "mc_bind", "mc_train_step", "mc_update_targets", "mc_policy",
-    "mc_copy_intermediate", "mc_set_timing", "mc_phase_times",
+    "mc_copy_intermediate", "mc_set_timing", "mc_phase_times", "mc_set_data_parallel",
 ]
+
+# mc_allreduce_fn (include/mc_coma.h): int (*)(float* buf, int64_t count, void* stream, void* ctx)
+MC_ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p)
 
 MC_P_COUNT = 6
 MC_NTAIL = 8
@@ -120,6 +123,7 @@ def load(required=True):
         "mc_copy_intermediate": ([vp, ctypes.c_int, vp, ctypes.POINTER(i64), vp], ctypes.c_int),
         "mc_set_timing": ([vp, i32], ctypes.c_int),
         "mc_phase_times": ([vp, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+        "mc_set_data_parallel": ([vp, MC_ALLREDUCE_FN, vp, i32, vp, i64], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

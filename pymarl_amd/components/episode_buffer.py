@@ -87,7 +87,7 @@ class EpisodeBatch:
             if k in self.data.transition_data:
                 target = self.data.transition_data
                 if mark_filled:
-                    target["filled"][slices] = 1
+                    target["filled"][tuple(slices)] = 1
                     mark_filled = False
                 _slices = tuple(slices)
             elif k in self.data.episode_data:

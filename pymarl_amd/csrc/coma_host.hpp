@@ -23,10 +23,32 @@ struct mc_handle {
   float *dL, *dHo, *pi, *ppart, *slab_fc2, *red_tmp, *norm_part;
   int last_T = 0, last_R = 0;
   bool timing = false;
+  // data parallel (mc_set_data_parallel)
+  mc_allreduce_fn dp_fn = nullptr;
+  void* dp_ctx = nullptr;
+  int dp_rank = 0;
+  float* dp_scratch = nullptr;
+  int64_t dp_scratch_n = 0;
+  std::vector<float> dp_msum;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 namespace {
+
+// One exchange step of the data-parallel mode: sum `n` floats at `buf` (caller-owned) over the ranks.
+int mc_allreduce(mc_handle* h, float* buf, int64_t n, hipStream_t s) {
+  if (h->dp_fn(buf, n, (void*)s, h->dp_ctx) != 0) return set_err(MQ_ERR_STATE, "data-parallel all-reduce callback failed");
+  return MQ_OK;
+}
+
+// Library-owned arrays travel through the caller's scratch buffer.
+int mc_allreduce_ws(mc_handle* h, float* ws_buf, int64_t n, hipStream_t s) {
+  MQ_HIP(hipMemcpyAsync(h->dp_scratch, ws_buf, n * sizeof(float), hipMemcpyDeviceToDevice, s));
+  int rc = mc_allreduce(h, h->dp_scratch, n, s);
+  if (rc) return rc;
+  MQ_HIP(hipMemcpyAsync(ws_buf, h->dp_scratch, n * sizeof(float), hipMemcpyDeviceToDevice, s));
+  return MQ_OK;
+}
 
 int mc_agent_config(const mc_config& c, mq_config* a) {
   std::memset(a, 0, sizeof(*a));
@@ -169,6 +191,12 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   MQ_HIP(hipMemsetAsync(h->cstate, 0, 4 * sizeof(int), s));
   hipLaunchKernelGGL(coma_mask_kernel, dim3((T + 255) / 256), dim3(256), 0, s, cd, rp, h->msum);
   MQ_HIP(hipGetLastError());
+  const bool dp = h->dp_fn != nullptr;
+  if (dp) {   // global per-step mask sums: every rank normalises by them and skips the same steps
+    if (h->dp_scratch_n < 8LL * T) return set_err(MQ_ERR_ARG, "data-parallel scratch smaller than 8 * t_len");
+    rc = mc_allreduce_ws(h, h->msum, T, s);
+    if (rc) return rc;
+  }
   hipLaunchKernelGGL(coma_xin_kernel, dim3(Tp * R), dim3(256), 0, s, cd, rp, h->X);
   MQ_HIP(hipGetLastError());
   // target critic over every stored step (coma_learner.py:102), then TD(lambda) (rl_utils.py:4-14)
@@ -205,18 +233,38 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   if (lds_l1 > 160 * 1024 || lds_head > 160 * 1024)
     return set_err(MQ_ERR_ARG, "critic input width or n_actions too large for the LDS-staged critic step");
   MQ_HIP(hipMemsetAsync(h->qvals, 0, (size_t)T * R * A * sizeof(float), s));   // skipped steps keep q_vals = 0
+  if (dp) {   // the host needs the live steps to place the per-step exchanges (one synchronisation per train)
+    h->dp_msum.resize(T);
+    MQ_HIP(hipMemcpyAsync(h->dp_msum.data(), h->msum, (size_t)T * sizeof(float), hipMemcpyDeviceToHost, s));
+    MQ_HIP(hipStreamSynchronize(s));
+  }
   if (h->timing) MQ_HIP(hipEventRecord(h->ev[1], s));
+  int live = 0;
   for (int t = T - 1; t >= 0; --t) {
-    const int Lexp = T - 1 - t;   // live steps before t when none was skipped
+    // live steps before t: exact in data-parallel mode, else assumed none was skipped (the kernels correct it)
+    const int Lexp = dp ? live : T - 1 - t;
     hipLaunchKernelGGL(coma_l1_kernel, dim3(ca.KS, CH / 16, (R + kL1Rows - 1) / kL1Rows), dim3(256), lds_l1, s, ca, t,
                        Lexp);
     hipLaunchKernelGGL(coma_head_kernel, dim3(ca.nhead), dim3(kHeadThreads), lds_head, s, ca, t, Lexp);
     hipLaunchKernelGGL(coma_wgrad_kernel, dim3(ca.nwgrad), dim3(256), 0, s, ca, t);
+    if (dp && h->dp_msum[t] > 0.0f) {   // sum the step's unnormalised gradient, then its norm from the sum
+      ++live;
+      MQ_HIP(hipGetLastError());
+      rc = mc_allreduce(h, h->cgrad, h->Pc, s);
+      if (rc) return rc;
+      hipLaunchKernelGGL(sumsq_kernel, dim3(ca.nwgrad), dim3(256), 0, s, (const float*)h->cgrad, h->Pc, h->cnorm);
+    }
   }
   MQ_HIP(hipGetLastError());
   hipLaunchKernelGGL(coma_capply_kernel, dim3((int)std::min<int64_t>((h->Pc + 255) / 256, 512)), dim3(256), 0, s,
                      ca);
   MQ_HIP(hipGetLastError());
+  if (dp) {   // per-step critic stat sums; the replicated fields (mask sum, norm, live flag) come from rank 0
+    if (h->dp_rank != 0) hipLaunchKernelGGL(coma_dp_crec_kernel, dim3((T + 255) / 256), dim3(256), 0, s, h->crec, T);
+    MQ_HIP(hipGetLastError());
+    rc = mc_allreduce_ws(h, h->crec, 8LL * T, s);
+    if (rc) return rc;
+  }
 
   if (h->timing) MQ_HIP(hipEventRecord(h->ev[2], s));
   // ---- actor: the agent unroll over t < T (coma_learner.py:52-57), online net only
@@ -306,6 +354,13 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
     MQ_HIP(hipGetLastError());
     nnorm = rb.b2;
   }
+  if (dp) {   // the agent gradient + loss / mask sums, then the norm partials of the summed gradient
+    rc = mc_allreduce(h, h->agrad, h->Pa + MQ_NSUMS, s);
+    if (rc) return rc;
+    nnorm = 256;
+    hipLaunchKernelGGL(sumsq_kernel, dim3(nnorm), dim3(256), 0, s, (const float*)h->agrad, h->Pa, h->norm_part);
+    MQ_HIP(hipGetLastError());
+  }
   {
     OptHP hp{c.lr, c.optim_alpha, c.optim_eps, c.grad_norm_clip, 1};
     const int blocks = (int)std::min<int64_t>((h->Pa + 255) / 256, 1024);
@@ -319,6 +374,19 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   if (h->timing) MQ_HIP(hipEventRecord(h->ev[3], s));
   h->last_T = T;
   h->last_R = R;
+  return MQ_OK;
+}
+
+int mc_set_data_parallel(mc_handle* h, mc_allreduce_fn allreduce, void* ctx, int32_t rank, float* scratch,
+                         int64_t scratch_count) {
+  if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
+  if (allreduce && (!scratch || scratch_count < 8LL * h->cfg.max_seq))
+    return set_err(MQ_ERR_ARG, "mc_set_data_parallel: scratch must hold 8 * max_seq floats");
+  h->dp_fn = allreduce;
+  h->dp_ctx = ctx;
+  h->dp_rank = rank;
+  h->dp_scratch = scratch;
+  h->dp_scratch_n = scratch_count;
   return MQ_OK;
 }
 

@@ -645,10 +645,12 @@ __global__ __launch_bounds__(256) void coma_wgrad_kernel(CritArgs a, int t) {
   } else if (tid == 0) {
     float* rec = a.crec + t * 8;
     for (int k = 0; k < 5; ++k) {
+      if (k == 1) continue;
       float s = 0.0f;
       for (int i = 0; i < a.nhead; ++i) s += a.cpart[i * 8 + k];
       rec[k] = s;
     }
+    rec[1] = a.msum[t];   // = the sum of the head partials [1] (integer-valued); the global one when data-parallel
     rec[6] = 1.0f;
     a.G[a.Pc] = a.msum[t];   // normaliser of the pending update
     a.cstate[0] += 1;
@@ -815,6 +817,13 @@ struct Dw2Prob {
     if (aa < A) slab[(int64_t)z * (A * H + A) + A * H + aa] = v;
   }
 };
+
+// Data-parallel ranks other than 0 zero the replicated fields of the per-step record (mask sum, grad norm, live flag)
+// before it is summed over the ranks, so the sum carries rank 0's values exactly.
+__global__ __launch_bounds__(256) void coma_dp_crec_kernel(float* __restrict__ crec, int T) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t < T) { crec[t * 8 + 1] = 0.0f; crec[t * 8 + 5] = 0.0f; crec[t * 8 + 6] = 0.0f; }
+}
 
 // Final stats (coma_learner.py:85-96): means of the per-step critic stats over the live steps in the order the
 // reference logs them (reversed t), then the actor's stats from the agent apply (stats[8..11] scratch on entry).

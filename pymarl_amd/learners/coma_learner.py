@@ -8,6 +8,11 @@ counterfactual baseline and the policy-gradient BPTT, both clips and both RMSpro
 hand-written HIP kernels (include/mc_coma.h, pymarl_amd/csrc/coma_kernels.hpp); torch only owns the buffers.
 There is no CPU path. One synchronisation per train(): the stats read-back the target update needs.
 
+Data parallel (not in the reference): with `args.learner_dp = True` and torch.distributed initialised,
+each rank trains its shard of the global sample and the library calls back into `dist.all_reduce` at every exchange
+step (the global per-step mask sums, each live critic step's gradient, the critic stat sums, the agent gradient);
+see include/mc_coma.h, mc_set_data_parallel. T = 180 critic steps mean 180 small all-reduces per train.
+
 Reference quirk kept on purpose: the actor reads `mac.action_selector.epsilon`, the value the last rollout call of
 select_actions left there (basic_controller.py:64-67).
 """
@@ -77,6 +82,9 @@ class COMALearner:
         self._handle = None
         self._handle_key = None
         self._steps = 0
+        self.dp = bool(getattr(args, "learner_dp", False))
+        self._dp_cb = None
+        self._dp_scratch = None
 
     # -- buffers ---------------------------------------------------------------------------------------------
     def _alloc_state(self, dev):
@@ -120,8 +128,33 @@ class COMALearner:
             P = _lib.ptr
             _lib.check(h.lib.mc_bind(h.h, P(self._agent), P(self._agrad), P(self._asq), P(self._critic),
                                      P(self._tcritic), P(self._cgrad), P(self._csq), P(self._stats)))
+            if self._dp_active():
+                self._dp_scratch = th.zeros(8 * T, dtype=th.float32, device=self._critic.device)
+                self._dp_cb = _lib.MC_ALLREDUCE_FN(self._allreduce)
+                import torch.distributed as dist
+                _lib.check(h.lib.mc_set_data_parallel(h.h, self._dp_cb, None, dist.get_rank(), P(self._dp_scratch),
+                                                      self._dp_scratch.numel()))
             self._handle, self._handle_key = h, (need_b, T)
         return self._handle
+
+    def _dp_active(self):
+        if not self.dp:
+            return False
+        import torch.distributed as dist
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+    def _allreduce(self, ptr, count, stream, ctx):
+        """mc_allreduce_fn: sum `count` floats of one of our own device buffers over the ranks, in stream order."""
+        try:
+            from .dp import allreduce_grad_buffer
+            for base in (self._cgrad, self._agrad, self._dp_scratch):
+                if base is not None and base.data_ptr() == ptr and count <= base.numel():
+                    allreduce_grad_buffer(base[:count])
+                    return 0
+            return 1
+        except Exception as e:   # an exception must not unwind through the C frames
+            self.logger.console_logger.error("COMA data-parallel all-reduce failed: %r", e)
+            return 1
 
     # -- reference API ---------------------------------------------------------------------------------------
     def train(self, batch, t_env: int, episode_num: int):

@@ -86,3 +86,76 @@ def test_two_rank_dp_equals_single_process(tmp_path):
     p0 = np.concatenate([v.ravel() for v in list(case.agent_params.values()) + list(case.mixer_params.values())])
     assert rel(dp["params"][0], p0 - 5e-4 * g / (np.sqrt(0.01 * g * g) + 1e-5)) < 1e-6
     assert np.abs(dp["params"][-1] - ref["params"][-1]).max() <= 20 * 5e-4
+
+
+# ---------------------------------------------------------------------------------------------------- COMA
+# Data-parallel COMA (include/mc_coma.h, mc_set_data_parallel): the library calls back into dist.all_reduce for the
+# global per-step mask sums, every live critic step's gradient (T per train), the critic stat sums and the agent
+# gradient. Two ranks on one GPU again; the single-process run on the whole batch is the reference.
+
+def _coma_train(learner, mac, buf, case, rank, world, steps, record):
+    from pymarl_amd.components.episode_buffer import SampledBatch
+    for k in range(steps):
+        gb = SampledBatch(buf, case.z["ids"][k])
+        gb = gb[:, :gb.max_t_filled()]
+        batch = gb.shard(rank, world) if world > 1 else gb
+        mac.action_selector.epsilon = case.epsilon[k]
+        learner.train(batch, 1000 * (k + 1), 8 * k)
+        st = learner.last_stats()
+        record["stats"].append([st[s] for s in COMA_DP_STATS])
+        record["critic"].append(learner._critic.detach().cpu().numpy().copy())
+        record["agent"].append(learner._agent.detach().cpu().numpy().copy())
+        record["agrad"].append(learner._agrad[:learner.n_agent_params].detach().cpu().numpy().copy())
+
+
+COMA_DP_STATS = ["critic_loss", "critic_grad_norm", "td_error_abs", "q_taken_mean", "target_mean", "advantage_mean",
+                 "coma_loss", "agent_grad_norm", "pi_max", "critic_steps", "mask_sum"]
+
+
+def _coma_worker(rank, world, port, name, steps, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    th.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tests.golden_utils import ComaCase
+        from tests.gpu_helpers import build_coma
+        case = ComaCase(name)
+        args, buf, mac, learner, logger = build_coma(case, learner_dp=True)
+        rec = {"stats": [], "critic": [], "agent": [], "agrad": []}
+        _coma_train(learner, mac, buf, case, rank, world, steps, rec)
+        th.cuda.synchronize()
+        if rank == 0:
+            np.savez(out_path, **{k: np.asarray(v) for k, v in rec.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,steps", [("coma_tiny", 3), ("coma_cfg5", 1)])
+def test_two_rank_coma_dp_equals_single_process(tmp_path, name, steps):
+    from tests.golden_utils import ComaCase
+    from tests.gpu_helpers import build_coma, rel
+    out = str(tmp_path / "coma_dp.npz")
+    mp.spawn(_coma_worker, args=(2, _free_port(), name, steps, out), nprocs=2, join=True)
+    dp = np.load(out)
+    case = ComaCase(name)
+    args, buf, mac, learner, logger = build_coma(case)
+    ref = {"stats": [], "critic": [], "agent": [], "agrad": []}
+    _coma_train(learner, mac, buf, case, 0, 1, steps, ref)
+
+    long_chain = case.T > 50
+    i_steps, i_msum = COMA_DP_STATS.index("critic_steps"), COMA_DP_STATS.index("mask_sum")
+    for k in range(steps):
+        a, b = dp["stats"][k], np.asarray(ref["stats"][k])
+        # every rank skips the same steps (global mask sums) and normalises by the global sum(mask)
+        assert a[i_steps] == b[i_steps] and a[i_msum] == b[i_msum], (k, a, b)
+        for j, s in enumerate(COMA_DP_STATS):
+            # T dependent critic steps: summation-order noise grows along the chain (cf. tests/test_gpu_coma.py);
+            # advantage_mean and coma_loss are sums that cancel, hence the absolute floor
+            tol = (2e-3 if long_chain else 1e-4) * abs(b[j]) + (2e-5 if long_chain else 1e-6)
+            assert abs(a[j] - b[j]) <= tol, (name, k, s, a[j], b[j])
+    # the critic takes T RMSprop steps per train: bound the parameters by O(lr) per element
+    assert np.abs(dp["critic"][-1] - ref["critic"][-1]).max() <= 20 * 5e-4
+    # the agent gradient reads the Q values of a critic that took T steps (cfg5: 180); the single-GPU test
+    # allows 5e-2 against the oracle for the same reason (tests/test_gpu_coma.py)
+    assert rel(dp["agrad"][0], ref["agrad"][0]) < (5e-3 if long_chain else 1e-4)
+    assert np.abs(dp["agent"][-1] - ref["agent"][-1]).max() <= 20 * 5e-4
