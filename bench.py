@@ -120,7 +120,7 @@ def build_workload(cfg_name, device, n_episodes=5000, unique=512, seed=0):
     return args, buf, learner, data
 
 
-def build_coma_workload(cfg_name, device, n_episodes=1000, unique=128, seed=0):
+def build_coma_workload(cfg_name, device, n_episodes=1000, unique=128, seed=0, dp=False):
     """COMALearner on an HBM-resident synthetic replay (coma_smac.yaml hyper-parameters)."""
     import torch as th
     from pymarl_amd.components.episode_buffer import ReplayBuffer
@@ -136,7 +136,7 @@ def build_coma_workload(cfg_name, device, n_episodes=1000, unique=128, seed=0):
               target_update_interval=200, learner_log_interval=10 ** 12, obs_last_action=True, obs_agent_id=True,
               agent="rnn", mac="basic_mac", agent_output_type="pi_logits", action_selector="multinomial",
               epsilon_start=0.5, epsilon_finish=0.01, epsilon_anneal_time=100000, mask_before_softmax=False,
-              batch_size=B, learner="coma_learner", device=str(device), use_cuda=True)
+              batch_size=B, learner="coma_learner", learner_dp=dp, device=str(device), use_cuda=True)
     scheme = {
         "state": {"vshape": S},
         "obs": {"vshape": O, "group": "agents"},
@@ -155,6 +155,7 @@ def build_coma_workload(cfg_name, device, n_episodes=1000, unique=128, seed=0):
             buf.data.transition_data[k][start:start + m] = th.as_tensor(v[:m], device=device)
     buf.episode_lengths[:] = buf.data.transition_data["filled"].sum(1).reshape(-1).cpu().numpy()
     buf.episodes_in_buffer = n_episodes
+    th.manual_seed(seed)   # identical random-init weights on every rank (data-parallel replicas start equal)
     mac = mac_REGISTRY["basic_mac"](buf.scheme, groups, args)
     learner = le_REGISTRY["coma_learner"](mac, buf.scheme, Logger(logging.getLogger("bench")), args)
     learner.cuda()
@@ -233,29 +234,65 @@ def coma_cpu_baseline(cfg_name, data, budget_s=12.0):
                       f"median {s * 1e3:.1f} ms/step, {cores} BLAS threads"}
 
 
-def coma_bench(a):
-    """cfg5: COMALearner.train on one GPU (the critic's T-step chain is a per-step exchange; DP COMA would need T
-    all-reduces per train, SURVEY.md §8e, and is not built: this line is N = 1)."""
+def init_distributed():
+    """One process per GPU (torch.distributed.run env); returns (world, rank, device)."""
     import torch as th
-    device = th.device("cuda", 0)
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # MQ_BENCH_BACKEND=gloo + more ranks than GPUs: rehearsal of the N>1 control flow on a 1-GPU box (ranks share
+    # devices round-robin; RCCL refuses two ranks on one GPU). The driver's N>1 runs use the default, RCCL.
+    backend = os.environ.get("MQ_BENCH_BACKEND", "nccl")
+    dev_index = local_rank % max(1, th.cuda.device_count())
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        th.cuda.set_device(dev_index)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=th.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
+    device = th.device("cuda", dev_index)
     th.cuda.set_device(device)
-    args, buf, learner, data, mac = build_coma_workload(a.config, device)
+    return world, rank, device
+
+
+def coma_bench(a):
+    """cfg5: COMALearner.train. N > 1 is data parallel with weak scaling (B = 8 episodes per rank): the critic's T
+    dependent optimiser steps make every live critic step an exchange, so each train() issues T + 3 all-reduces
+    (include/mc_coma.h, mc_set_data_parallel; SURVEY.md §8e "COMA caveat")."""
+    import torch as th
+    import torch.distributed as dist
+    world, rank, device = init_distributed()
+    args, buf, learner, data, mac = build_coma_workload(a.config, device, dp=world > 1)
     _, n, A, O, S, T, B, desc = CONFIGS[a.config]
     np.random.seed(2)
 
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
     def step(k):
-        b = buf.sample(B)
+        gb = buf.sample(B * world)
+        b = gb.shard(rank, world) if world > 1 else gb
         mac.action_selector.epsilon = mac.action_selector.schedule.eval(1000 * k)
         learner.train(b[:, :b.max_t_filled()], 1000 * k, 8 * k)
 
     for k in range(max(1, a.warmup)):
         step(k)
     th.cuda.synchronize()
+    barrier()
+    th.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(a.steps):
         step(k)
     th.cuda.synchronize()
+    barrier()
     dt = time.perf_counter() - t0
+    if world > 1:
+        t = th.tensor([dt], dtype=th.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
     learner.set_timing(True)
     chains = []
     for k in range(min(a.steps, 20)):
@@ -267,15 +304,18 @@ def coma_bench(a):
     R = B * n
     step_flops = 2 * R * (2 * Kc * 128 + 3 * 128 * 128 + 2 * 128 * A)   # one critic step, fwd + bwd
     achieved = step_flops / (chain_ms * 1e-3 / T) / 1e12
-    value = B * T * n * a.steps / dt
-    cpu = None if a.no_cpu_baseline else coma_cpu_baseline(a.config, data)
+    value = B * T * n * world * a.steps / dt
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    cpu = None if (a.no_cpu_baseline or world > 1) else coma_cpu_baseline(a.config, data)
     line = {
-        "metric": METRIC, "value": value, "unit": "samples/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "metric": METRIC, "value": value, "unit": "samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32", "data": "synthetic (SURVEY.md §8d replay recipe, random-init weights)",
         "config": {"workload": desc, "learner": "coma_learner", "n_agents": n, "n_actions": A, "obs_dim": O,
-                   "state_dim": S, "episode_limit": T, "batch_per_gpu": B, "global_batch": B,
-                   "replay_episodes": buf.buffer_size, "parallelism": "dp1"},
+                   "state_dim": S, "episode_limit": T, "batch_per_gpu": B, "global_batch": B * world,
+                   "replay_episodes": buf.buffer_size, "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": "critic step chain (l1 + head + wgrad, x T)",
                      "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "launch_ms": chain_ms / T,
@@ -284,6 +324,8 @@ def coma_bench(a):
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def pmc_traffic(cfg_name, phase):
@@ -316,23 +358,7 @@ def main():
     import torch as th
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # MQ_BENCH_BACKEND=gloo + more ranks than GPUs: rehearsal of the N>1 control flow on a 1-GPU box (ranks share
-    # devices round-robin; RCCL refuses two ranks on one GPU). The driver's N>1 runs use the default, RCCL.
-    backend = os.environ.get("MQ_BENCH_BACKEND", "nccl")
-    dev_index = local_rank % max(1, th.cuda.device_count())
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        th.cuda.set_device(dev_index)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=th.device("cuda", dev_index))
-        else:
-            dist.init_process_group(backend)
-    device = th.device("cuda", dev_index)
-    th.cuda.set_device(device)
-
+    world, rank, device = init_distributed()
     args, buf, learner, data = build_workload(a.config, device)
     mixer, n, A, O, S, T, B, desc = CONFIGS[a.config]
 
