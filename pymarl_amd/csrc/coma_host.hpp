@@ -278,7 +278,7 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   const float* Pa = h->agent;
   const int rw_fwd = pick_rw(d.R, 512);
   if (rw_fwd == 1 && fused_fwd_ok(d.I, d.O, d.A, d.n, RT)) {
-    hipLaunchKernelGGL(gru_fwd_fused_kernel<0>, dim3(d.R, 1), dim3(512), 0, s, d, rp, Pa, Pa, L, w);
+    launch_fwd_fused(dim3(d.R, 1), s, d, rp, Pa, Pa, L, w);
     MQ_HIP(hipGetLastError());
   } else {
     Fc1Prob p1{d, rp, Pa, Pa, ah->off[MQ_P_FC1_W], ah->off[MQ_P_FC1_B], w.X1, w.XIN, RT};

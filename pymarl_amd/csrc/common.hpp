@@ -42,6 +42,23 @@ MQ_DEV uint32_t fdiv(uint32_t x, const FastDiv& f) {
   return (t + x) >> f.shift;
 }
 
+// Global access as a wave-uniform base plus a 32-bit per-lane ELEMENT offset: the byte offset is formed in 32 bits
+// and zero-extended, which is the pattern the backend lowers to one saddr load / store (SGPR base + VGPR offset)
+// instead of 64-bit VALU address math. The caller guarantees elem * 4 < 2^32.
+MQ_DEV float ld_u32(const float* base, uint32_t elem) { return *(const float*)((const char*)base + (elem << 2)); }
+MQ_DEV void st_u32(float* base, uint32_t elem, float v) { *(float*)((char*)base + (elem << 2)) = v; }
+
+// Raw buffer stores through a wave-uniform descriptor with a 32-bit per-lane byte offset. An offset of kDrop lies
+// past num_records, so the hardware range check drops that lane's store: predicated stores without exec-mask
+// branches (which split live ranges and cost register shuffles in the register-capped fused kernels).
+constexpr uint32_t kDrop = 0xFFFFFFF0u;
+MQ_DEV __amdgpu_buffer_rsrc_t buf_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7FFFFFF0, 0x00020000);
+}
+MQ_DEV void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, byte_off, 0, 0);
+}
+
 // Lane exchange inside an aligned group of 4 lanes (DPP quad_perm, no LDS round trip).
 MQ_DEV float quad_xor1(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));

@@ -159,6 +159,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     lds_barrier();
     lookup_w2(sa);
     int t = Tp - 1;
+    if (VAR & 128) __builtin_amdgcn_s_setprio(2);
     if (VAR & 8) {   // diagnostic only: chain cycles per step, binned by the producer phase u = 15 - (t & 15)
       uint64_t bins[FCH];
 #pragma unroll
@@ -189,6 +190,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       }
       if (t >= 0) step(t, sa, sb);
     }
+    if (VAR & 128) __builtin_amdgcn_s_setprio(0);
     lds_barrier();   // producer tail: chunk 0 (2 barriers)
     lds_barrier();
     if (q < 3) { slab[o_bi + q * H + k] = db_i; slab[o_bh + q * H + k] = db_h; }

@@ -21,6 +21,7 @@
 // B[kk = g][j = c], D[i = 4g + reg][j = c]. Lane group g owns a contiguous quarter of K (k = g * Kq + kb), so
 // A and B fragments are row-contiguous LDS reads (W_ih's fragments stay in VGPRs).
 #pragma once
+#include <cstdlib>
 #include "gru_kernels.hpp"
 
 namespace mq {
@@ -56,9 +57,13 @@ struct FusedLds {
 };
 
 // VAR: ablation bits for scripts/rec_micro.hip only (production = 0): 1 skip Hs/Gates stores, 2 stamp the T loop,
+// 128 chain waves without priority, 256 gathers two chunks ahead, 512 producer work spread over all 16 phases,
+// 1024 target chain above the online chain,
 // 4 producers idle (recurrence alone on stale gates), 8 per-phase cycle bins, 16 no obs loads, 32 no X1/XIN stores,
 // 64 prologue milestone stamps.
-template <int VAR = 0>
+// NG: obs gather slots per producer thread (16 * O <= 256 * NG); the host picks the smallest instantiation
+// (launch_fwd_fused) because every slot holds two VGPRs across the whole T loop.
+template <int VAR = 0, int NG = FGATHER>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void gru_fwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P0,
                                                                const float* __restrict__ P1, Lay L, Work w) {
   __shared__ FusedLds S;
@@ -70,13 +75,54 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const int R = d.R, Tp = d.Tp, I = d.I, O = d.O, A = d.A, n = d.n;
   const int cl = (Tp - 1) / FCH;   // last chunk
   const int r = blockIdx.x;
+  // Output addressing: a wave-uniform base (SGPR pointer) plus a 32-bit per-lane offset, so every global access is
+  // one saddr load / store with no 64-bit VALU address math.
+  const uint32_t RH = (uint32_t)R * H;
 
-  // ---- shared prologue: weights to LDS (all loads in flight before the first store), zero padding, h0
-  if ((VAR & 64) && tid == 256)
-    ((uint64_t*)w.slab_mix)[16 * (blockIdx.y * gridDim.x + blockIdx.x)] = __builtin_amdgcn_s_memrealtime();
-  {
-    constexpr int N1 = (H * FXP + 511) / 512, N2 = (16 * (H + 4) + 511) / 512;
-    float v1[N1], v2[N2];
+  // ---- producer addressing, and chunk 0's obs gather issued first: its HBM round trip overlaps the weight loads
+  const int ptid = tid - 256;   // producer thread id (negative in the recurrence waves, which never use it)
+  // replay addressing of this row (r = b * n + agent)
+  const int b = (int)fdiv((uint32_t)r, d.dN), ag = r - b * n;
+  const int64_t slot0 = rp.ep(b) * d.t_stride;
+  const float* obs_row = rp.obs + (slot0 * n + ag) * (int64_t)O;   // + t * n * O
+  float* X1o = w.X1;     // online X1 [RT][H]
+  float* XINo = w.XIN;   // online XIN [RT][I]
+  float* Qz = w.Q + (int64_t)z * d.RT() * A;
+  const uint32_t RI = (uint32_t)R * I, RA = (uint32_t)R * A;
+
+  // gather slot s: element e = ptid + 256 s of the chunk's [16][O] obs block -> (row i, column), packed once as
+  // (i << 28) | (column << 20) | (i * n * O + column) (the last field: the element's offset from the chunk's first
+  // obs row, < 2^20 since n * O < 2^16); -1 past the block
+  int gsl[NG];
+#pragma unroll
+  for (int s = 0; s < NG; ++s) {
+    const int e = ptid + 256 * s, i = (int)fdiv((uint32_t)e, d.dO), col = e - i * O;
+    gsl[s] = e < FCH * O ? (i << 28) | (col << 20) | (i * n * O + col) : -1;
+  }
+  const int nO = n * O;
+  float xr[NG];
+  int f_ld = 0, a_ld = -1;   // low words of filled[t-1] / actions[t-1] (int64, little-endian, small values)
+  auto issue_gather = [&](int cc) {
+    const int t0 = FCH * cc;
+    // unconditional loads from clamped addresses (no exec-masked branches); out-of-range slots are zeroed when
+    // stored (store_gather)
+    const float* base = obs_row + (int64_t)t0 * nO;
+    const int lim = (Tp - 1 - t0) * nO + O - 1;   // last valid element offset of this chunk
+#pragma unroll
+    for (int s = 0; s < NG; ++s)
+      xr[s] = (VAR & 16) ? (float)s : ld_u32(base, (uint32_t)min(opaque(gsl[s]) & 0xFFFFF, lim));
+    {
+      const int t = min(max(t0 + (ptid & (FCH - 1)), 1), Tp - 1) - 1;
+      f_ld = *(const int*)(rp.filled + slot0 + t);
+      a_ld = *(const int*)(rp.actions + (slot0 + t) * n + ag);
+    }
+  };
+  // ---- prologue: every global load of a role (shared LDS weights, its own register-resident weights, and for the
+  // producers chunk 0's obs gather first) is in flight before the first LDS store: one HBM round trip. The shared
+  // part runs inside each role's branch so the two roles' register weights never share a live range.
+  constexpr int N1 = (H * FXP + 511) / 512, N2 = (16 * (H + 4) + 511) / 512;
+  float v1[N1], v2[N2];
+  auto shared_load = [&]() {
 #pragma unroll
     for (int u = 0; u < N1; ++u) {
       const int e = tid + 512 * u, nn = e / FXP, k = e - nn * FXP;
@@ -87,6 +133,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const int e = tid + 512 * u, a = e / (H + 4), k = e - a * (H + 4);
       v2[u] = (e < 16 * (H + 4) && a < A && k < H) ? P[L.o[MQ_P_FC2_W] + (int64_t)a * H + k] : 0.0f;
     }
+  };
+  auto shared_store = [&]() {   // fc1 / fc2 weights to LDS, zero padding, h0
 #pragma unroll
     for (int u = 0; u < N1; ++u) {
       const int e = tid + 512 * u;
@@ -97,14 +145,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const int e = tid + 512 * u;
       if (e < 16 * (H + 4)) (&S.w2[0][0])[e] = v2[u];
     }
-  }
-  for (int e = tid; e < FCH * FXP; e += 512) (&S.xin[0][0])[e] = 0.0f;
-  if (tid < H) S.h0[tid] = 0.0f;   // init_hidden: h0 = 0
+    for (int e = tid; e < FCH * FXP; e += 512) (&S.xin[0][0])[e] = 0.0f;
+    if (tid < H) S.h0[tid] = 0.0f;   // init_hidden: h0 = 0
+  };
+  if ((VAR & 64) && tid == 256)
+    ((uint64_t*)w.slab_mix)[16 * (blockIdx.y * gridDim.x + blockIdx.x)] = __builtin_amdgcn_s_memrealtime();
 
   if (rec) {
     // ================================================================ recurrence waves
     const int j = tid >> 2, q = tid & 3;
     f32x2 wr[8], wz[8], wn[8];   // W_hh[gate * 64 + j][16 q .. 16 q + 15] as pairs for v_pk_fma_f32
+    shared_load();
     {
       const float* Whh = P + L.o[MQ_P_RNN_W_HH];
 #pragma unroll
@@ -116,6 +167,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     }
     const float bhr = P[L.o[MQ_P_RNN_B_HH] + j], bhz = P[L.o[MQ_P_RNN_B_HH] + H + j],
                 bhn = P[L.o[MQ_P_RNN_B_HH] + 2 * H + j];
+    shared_store();
     drain_vmem();
     for (int i = 0; i < 5; ++i) lds_barrier();   // the producers' chunk-0 prologue (5 barriers)
     float* Hz = w.Hs;   // online only: the backward pass reads h_{t-1}
@@ -125,6 +177,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const float m3 = q == 3 ? 1.0f : 0.0f;
     const float bsel = m0 * bhr + m1 * bhz;
     float hprev = 0.0f;   // h_{t-1}[j]: every lane of the quad computes unit j's h, so it never re-reads LDS
+    const uint32_t hlo = q == 0 ? ((uint32_t)r * H + j) * 4 : kDrop, glo = ((uint32_t)r * (4 * H) + q * H + j) * 4;
     auto step = [&](int t) {
       const int p = t & (FCH - 1), c = t / FCH;
       const float* hb = t == 0 ? S.h0 : S.hs[((t - 1) / FCH) & 1][(t - 1) & (FCH - 1)];
@@ -155,12 +208,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       hprev = h1;
       if (q == 0) S.hs[c & 1][p][j] = h1;
       if (online && !(VAR & 1)) {
-        const int64_t tr = (int64_t)t * R + r;
-        if (q == 0) Hz[tr * H + j] = h1;
-        w.Gates[tr * (4 * H) + q * H + j] = fmaf(m0, rg, fmaf(m1, zg, fmaf(m2, ng, m3 * ghn)));
+        buf_st(buf_rsrc(Hz + (int64_t)t * RH), hlo, h1);   // wave-uniform bases; lanes q != 0 drop the h store
+        buf_st(buf_rsrc(w.Gates + (int64_t)t * (4 * RH)), glo, fmaf(m0, rg, fmaf(m1, zg, fmaf(m2, ng, m3 * ghn))));
       }
       lds_barrier();
     };
+    // the chains of both nets issue ahead of every producer wave on the CU (the online workgroups are older and
+    // would otherwise win arbitration against the target chain too); VAR 128 turns this off for A/B runs
+    if (VAR & 1024) {
+      if (online) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(3);
+    }
+    else if (!(VAR & 128)) __builtin_amdgcn_s_setprio(2);
     uint64_t c0 = 0, r0t = 0;
     if (VAR & 2) { c0 = __builtin_amdgcn_s_memtime(); r0t = __builtin_amdgcn_s_memrealtime(); }
     if (VAR & 8) {   // diagnostic only: shader cycles per step phase p, summed over the chunks
@@ -183,6 +242,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     } else {
       for (int t = 0; t < Tp; ++t) step(t);
     }
+    __builtin_amdgcn_s_setprio(0);
     if ((VAR & 2) && tid == 0) {   // diagnostic only: shader cycles and 100 MHz ticks of the whole T loop
       const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
       ((uint64_t*)w.slab_mix)[2 * (blockIdx.y * gridDim.x + blockIdx.x)] = c1 - c0;
@@ -192,8 +252,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   }
 
   // ================================================================== producer waves
-  const int ptid = tid - 256, wv = ptid >> 6, lane = ptid & 63, g = lane >> 4, c16 = lane & 15;
+  const int wv = ptid >> 6, lane = ptid & 63, g = lane >> 4, c16 = lane & 15;
   const int Kq = (I + 15) / 16 * 4;   // k-blocks per lane group (multiple of 4: b128 operand reads)
+  issue_gather(0);
+  shared_load();
   float wih[3][16], bih[3];
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
@@ -205,66 +267,37 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   }
   const float b1 = P[L.o[MQ_P_FC1_B] + 16 * wv + c16];
   const float b2 = c16 < A ? P[L.o[MQ_P_FC2_B] + c16] : 0.0f;
+  shared_store();
 
-  // replay addressing of this row (r = b * n + agent)
-  const int b = (int)fdiv((uint32_t)r, d.dN), ag = r - b * n;
-  const int64_t slot0 = rp.ep(b) * d.t_stride;
-  const float* obs_row = rp.obs + (slot0 * n + ag) * (int64_t)O;   // + t * n * O
-  float* X1o = w.X1;     // online X1 [RT][H]
-  float* XINo = w.XIN;   // online XIN [RT][I]
-  float* Qz = w.Q + (int64_t)z * d.RT() * A;
-
-  // gather slot s: element e = ptid + 256 s of the chunk's [16][O] obs block -> (row i, column), packed once as
-  // (i << 16) | (i * n * O + column) (the element's offset from the chunk's first obs row); -1 past the block
-  int gsl[FGATHER];
-#pragma unroll
-  for (int s = 0; s < FGATHER; ++s) {
-    const int e = ptid + 256 * s, i = (int)fdiv((uint32_t)e, d.dO);
-    gsl[s] = e < FCH * O ? (i << 16) | (i * n * O + e - i * O) : -1;
-  }
-  const int nO = n * O;
-  float xr[FGATHER];
-  int f_ld = 0, a_ld = -1;   // low words of filled[t-1] / actions[t-1] (int64, little-endian, small values)
-  auto issue_gather = [&](int cc) {
+  auto store_gather = [&](int cc, int s0 = 0, int s1 = NG) {
     const int t0 = FCH * cc;
-    // unconditional loads from clamped addresses (no exec-masked branches); out-of-range slots are zeroed when
-    // stored (store_gather)
-    const float* base = obs_row + (int64_t)t0 * nO;
-    const int lim = (Tp - 1 - t0) * nO + O - 1;   // last valid element offset of this chunk
+    const auto xr_rsrc = buf_rsrc(XINo + ((int64_t)t0 * R + r) * I);   // wave-uniform
 #pragma unroll
-    for (int s = 0; s < FGATHER; ++s) xr[s] = (VAR & 16) ? (float)s : base[min(opaque(gsl[s]) & 0xFFFF, lim)];
-    {
-      const int t = min(max(t0 + (ptid & (FCH - 1)), 1), Tp - 1) - 1;
-      f_ld = *(const int*)(rp.filled + slot0 + t);
-      a_ld = *(const int*)(rp.actions + (slot0 + t) * n + ag);
-    }
-  };
-  auto store_gather = [&](int cc) {
-    const int t0 = FCH * cc;
-    float* xg = XINo + ((int64_t)t0 * R + r) * I;
-#pragma unroll
-    for (int s = 0; s < FGATHER; ++s) {
+    for (int s = 0; s < NG; ++s) {
+      if (s < s0 || s >= s1) continue;
       const int gs = opaque(gsl[s]);
-      if (gs < 0) continue;
-      const int i = gs >> 16, col = (gs & 0xFFFF) - i * nO;
-      const bool ok = t0 + i < Tp;
-      S.xin[i][col] = ok ? xr[s] : 0.0f;
-      if (online && ok && !(VAR & 32)) xg[i * R * I + col] = xr[s];   // RT * I < 2^31 (host check)
+      const int i = (int)((uint32_t)gs >> 28), col = (gs >> 20) & 0xFF;
+      const bool live = gs != -1, ok = live && t0 + i < Tp;   // (i >= 8 sets the sign bit: compare with -1)
+      // a slot past the block writes the never-read pad column xin[0][FXP - 1] and drops its global store
+      (&S.xin[0][0])[live ? i * FXP + col : FXP - 1] = ok ? xr[s] : 0.0f;
+      if (online && !(VAR & 32)) buf_st(xr_rsrc, ok ? ((uint32_t)i * RI + col) * 4 : kDrop, xr[s]);
     }
     // actions_onehot[t-1] is zero unless slot t-1 was filled (runner contract)
-    if (ptid < FCH) {
+    if (s1 == NG && ptid < FCH) {
       const int t = t0 + ptid;
       S.aprev[ptid] = (d.last_action && t > 0 && t < Tp && f_ld) ? a_ld : -1;
     }
   };
   auto onehots = [&](int cc) {
     const int t0 = FCH * cc, wd = I - O, i = ptid >> 4, t = t0 + i;
+    const auto xo = buf_rsrc(XINo + ((int64_t)t0 * R + r) * I + O);   // wave-uniform
+    const uint32_t ro = (uint32_t)i * RI;
     for (int col = ptid & 15; col < wd; col += 16) {
       float v;
       if (d.last_action && col < A) v = col == S.aprev[i] ? 1.0f : 0.0f;
       else v = (col - (d.last_action ? A : 0)) == ag ? 1.0f : 0.0f;
       S.xin[i][O + col] = v;
-      if (online && t < Tp && !(VAR & 32)) XINo[((int64_t)t * R + r) * I + O + col] = v;
+      if (online && !(VAR & 32)) buf_st(xo, t < Tp ? (ro + col) * 4 : kDrop, v);   // rows past Tp drop
     }
   };
   f32x4 acc1 = {0, 0, 0, 0}, acc1b = {0, 0, 0, 0}, accg[3] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -282,12 +315,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   };
   auto fc1_epi = [&](int cc) {
     const int t0 = FCH * cc;
+    const auto xb = buf_rsrc(X1o + ((int64_t)t0 * R + r) * H);   // wave-uniform
+    const uint32_t lo = (uint32_t)(4 * g) * RH + 16 * wv + c16;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int i = 4 * g + e, t = t0 + i;
       const float x = fmaxf((acc1[e] + acc1b[e]) + b1, 0.0f);
       S.x1[i][16 * wv + c16] = x;
-      if (online && t < Tp && !(VAR & 32)) X1o[((int64_t)t * R + r) * H + 16 * wv + c16] = x;
+      if (online && !(VAR & 32)) buf_st(xb, t < Tp ? (lo + e * RH) * 4 : kDrop, x);
     }
     acc1 = f32x4{0, 0, 0, 0};
     acc1b = f32x4{0, 0, 0, 0};
@@ -323,12 +358,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   auto fc2_store = [&](int cc) {
     if (wv != 0) return;
     const int t0 = FCH * cc;
+    const auto qb = buf_rsrc(Qz + ((int64_t)t0 * R + r) * A);   // wave-uniform
+    const uint32_t lo = (uint32_t)(4 * g) * RA + c16;
+    float v[4];   // every LDS read first, then the stores
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int i = 4 * g + e, t = t0 + i;
-      const float v = ((qpart[0][i][c16] + qpart[1][i][c16]) + (qpart[2][i][c16] + qpart[3][i][c16])) + b2;
-      if (t < Tp && c16 < A) Qz[((int64_t)t * R + r) * A + c16] = v;
+      const int i = 4 * g + e;
+      v[e] = ((qpart[0][i][c16] + qpart[1][i][c16]) + (qpart[2][i][c16] + qpart[3][i][c16])) + b2;
     }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      buf_st(qb, (t0 + 4 * g + e < Tp && c16 < A) ? (lo + e * RA) * 4 : kDrop, v[e]);
   };
 
   // chunk 0 synchronously (5 barriers, matched by the recurrence waves)
@@ -337,8 +377,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     if ((VAR & 64) && ptid == 0) stp[k] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(1);
-  issue_gather(0);
-  drain_vmem();
+  drain_vmem();   // chunk 0's gather (issued before the weight loads)
   stamp(2);
   lds_barrier();   // 1: weights, padding staged
   stamp(3);
@@ -353,6 +392,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   stamp(5);
   gi_part(0, 16);
   gi_epi(0);
+  if ((VAR & 512) && cl >= 1) issue_gather(1);
   lds_barrier();   // 5
   stamp(6);
 
@@ -363,10 +403,35 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
       for (int p = 0; p < FCH; ++p) {
         if (t0 + p >= Tp) continue;   // last chunk: no work past Tp (no work for chunk c+1 either)
+        if (VAR & 512) {
+          // rebalanced: producer work in every phase, gathers two chunks ahead
+          if (p == 0 && c >= 1) fc2_partial(c - 1);
+          if (p == 1 && c >= 1) fc2_store(c - 1);
+          if (next) {
+            if (p == 2) store_gather(c + 1, 0, 3);
+            if (p == 3) store_gather(c + 1, 3, NG);
+            if (p == 4) onehots(c + 1);
+            if (p == 5) { fc1_part(0, 2); if (c + 2 <= cl) issue_gather(c + 2); }
+            if (p == 6) fc1_part(2, 4);
+            if (p == 7) fc1_part(4, 6);
+            if (p == 8) { fc1_part(6, 8); fc1_epi(c + 1); }
+            if (p == 9) gi_part(0, 3);
+            if (p == 10) gi_part(3, 5);
+            if (p == 11) gi_part(5, 7);
+            if (p == 12) gi_part(7, 9);
+            if (p == 13) gi_part(9, 11);
+            if (p == 14) gi_part(11, 13);
+            if (p == 15) { gi_part(13, 16); gi_epi(c + 1); }
+          }
+          lds_barrier();
+          continue;
+        }
         if (p == 0) {
           if (c >= 1) fc2_partial(c - 1);
-          if (next) issue_gather(c + 1);
+          if (next && (!(VAR & 256) || c == 0)) issue_gather(c + 1);
         }
+        // VAR 256: chunk c+2's gather right after chunk c+1's was staged (15 steps of latency instead of 5)
+        if ((VAR & 256) && p == 6 && c + 2 <= cl) issue_gather(c + 2);
         if (p == 1 && c >= 1) fc2_store(c - 1);
         if (next) {
           if (p == 5) store_gather(c + 1);
@@ -410,6 +475,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     }
   }
   stamp(8);
+}
+
+// Host: the fused forward with the smallest gather-slot instantiation that covers O.
+template <int VAR = 0>
+inline void launch_fwd_fused_v(dim3 grid, hipStream_t s, const Dims& d, const Rep& rp, const float* P0,
+                               const float* P1, const Lay& L, const Work& w) {
+  if (FCH * d.O <= 256 * 5)
+    hipLaunchKernelGGL((gru_fwd_fused_kernel<VAR, 5>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
+  else
+    hipLaunchKernelGGL((gru_fwd_fused_kernel<VAR, FGATHER>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
+}
+// MQ_FWD_VAR (A/B runs of the schedule variants in the real pipeline, where the obs gather reads cold HBM):
+// 256 gathers two chunks ahead, 512 the rebalanced schedule. Unset = production.
+inline void launch_fwd_fused(dim3 grid, hipStream_t s, const Dims& d, const Rep& rp, const float* P0, const float* P1,
+                             const Lay& L, const Work& w) {
+  static const int var = [] { const char* e = std::getenv("MQ_FWD_VAR"); return e ? std::atoi(e) : 0; }();
+  if (var == 256) launch_fwd_fused_v<256>(grid, s, d, rp, P0, P1, L, w);
+  else if (var == 512) launch_fwd_fused_v<512>(grid, s, d, rp, P0, P1, L, w);
+  else if (var == 16) launch_fwd_fused_v<16>(grid, s, d, rp, P0, P1, L, w);    // diagnostic: no obs loads
+  else if (var == 32) launch_fwd_fused_v<32>(grid, s, d, rp, P0, P1, L, w);    // diagnostic: no X1 / XIN stores
+  else if (var == 128) launch_fwd_fused_v<128>(grid, s, d, rp, P0, P1, L, w);  // no chain priority
+  else launch_fwd_fused_v<0>(grid, s, d, rp, P0, P1, L, w);
 }
 
 }  // namespace mq

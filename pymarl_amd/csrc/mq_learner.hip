@@ -369,8 +369,7 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   if (rw_fwd == 1 && fused_fwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused) {
     // one row per workgroup: fc1 / W_ih / fc2 ride on the recurrence's idle matrix cores (gru_fwd_fused.hpp)
     pt.begin(PH_GRUF);
-    hipLaunchKernelGGL(gru_fwd_fused_kernel<0>, dim3(d.R, 2), dim3(512), 0, s, d, rp, (const float*)h->on,
-                       (const float*)h->tg, L, w);
+    launch_fwd_fused(dim3(d.R, 2), s, d, rp, (const float*)h->on, (const float*)h->tg, L, w);
     MQ_HIP(hipGetLastError());
   } else {
     pt.begin(PH_FC1);

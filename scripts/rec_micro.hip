@@ -104,24 +104,64 @@ int main(int argc, char** argv) {
     auto runf = [&](auto kern) {
       return time_it([&] { hipLaunchKernelGGL(kern, dim3(d.R, 2), dim3(512), 0, 0, d, rf, (const float*)P0, (const float*)P1, L, w); });
     };
-    printf("fused fwd %.1f us\n", runf(gru_fwd_fused_kernel<0>));
-    printf("fused fwd V1(no Hs/Gates st) %.1f us\n", runf(gru_fwd_fused_kernel<1>));
-    printf("fused fwd V4(no chunk pipeline) %.1f us\n", runf(gru_fwd_fused_kernel<4>));
-    printf("fused fwd V5 %.1f us\n", runf(gru_fwd_fused_kernel<5>));
-    runf(gru_fwd_fused_kernel<2>);
+    printf("fused fwd %.1f us\n", runf(gru_fwd_fused_kernel<0, 5>));
+    {  // interleaved rounds (one process): median / min per variant
+      const char* names[] = {"V0", "V128 prio", "V512 rebal", "V640 prio+rebal", "V1536 tprio+rebal"};
+      std::vector<std::vector<float>> ts(5);
+      for (int round = 0; round < 9; ++round) {
+        ts[0].push_back(runf(gru_fwd_fused_kernel<0, 5>));
+        ts[1].push_back(runf(gru_fwd_fused_kernel<128, 5>));
+        ts[2].push_back(runf(gru_fwd_fused_kernel<512, 5>));
+        ts[3].push_back(runf(gru_fwd_fused_kernel<640, 5>));
+        ts[4].push_back(runf(gru_fwd_fused_kernel<1536, 5>));
+      }
+      for (int v = 0; v < 5; ++v) {
+        std::sort(ts[v].begin(), ts[v].end());
+        printf("fused fwd %-20s median %.1f us min %.1f us\n", names[v], ts[v][ts[v].size() / 2], ts[v][0]);
+      }
+    }
+    printf("fused fwd V1(no Hs/Gates st) %.1f us\n", runf(gru_fwd_fused_kernel<1, 5>));
+    printf("fused fwd V4(no chunk pipeline) %.1f us\n", runf(gru_fwd_fused_kernel<4, 5>));
+    printf("fused fwd V5 %.1f us\n", runf(gru_fwd_fused_kernel<5, 5>));
+    printf("fused fwd V128(chain prio) %.1f us\n", runf(gru_fwd_fused_kernel<128, 5>));
+    printf("fused fwd V256(early gather) %.1f us\n", runf(gru_fwd_fused_kernel<256, 5>));
+    printf("fused fwd V384(both) %.1f us\n", runf(gru_fwd_fused_kernel<384, 5>));
+    printf("fused fwd V640(prio+rebalanced) %.1f us\n", runf(gru_fwd_fused_kernel<640, 5>));
+    printf("fused fwd V512(rebalanced) %.1f us\n", runf(gru_fwd_fused_kernel<512, 5>));
+    printf("fused fwd V1536(target prio+rebalanced) %.1f us\n", runf(gru_fwd_fused_kernel<1536, 5>));
+    printf("fused fwd V1280(target prio+early) %.1f us\n", runf(gru_fwd_fused_kernel<1280, 5>));
+    for (int var : {130, 258, 642, 1538}) {
+      if (var == 130) runf(gru_fwd_fused_kernel<130, 5>);
+      else if (var == 258) runf(gru_fwd_fused_kernel<258, 5>);
+      else if (var == 642) runf(gru_fwd_fused_kernel<642, 5>);
+      else runf(gru_fwd_fused_kernel<1538, 5>);
+      std::vector<uint64_t> sv(2 * 2 * d.R);
+      CK(hipMemcpy(sv.data(), w.slab_mix, sv.size() * 8, hipMemcpyDeviceToHost));
+      for (int net = 0; net < 2; ++net) {
+        double cn = 0;
+        for (int i = net * d.R; i < (net + 1) * d.R; ++i) cn += sv[2 * i];
+        printf("  V%d net %d loop: %.0f cycles/step\n", var, net, cn / d.R / d.Tp);
+      }
+    }
+    runf(gru_fwd_fused_kernel<2, 5>);
     std::vector<uint64_t> st(2 * 2 * d.R);
     CK(hipMemcpy(st.data(), w.slab_mix, st.size() * 8, hipMemcpyDeviceToHost));
     double cyc = 0, tick = 0;
     for (int i = 0; i < 2 * d.R; ++i) { cyc += st[2 * i]; tick += st[2 * i + 1]; }
     cyc /= 2 * d.R; tick /= 2 * d.R;
     printf("fused fwd stamped: %.0f cycles/step, %.3f us/step\n", cyc / d.Tp, tick / 100.0 / d.Tp);
-    runf(gru_fwd_fused_kernel<6>);
+    for (int net = 0; net < 2; ++net) {
+      double cn = 0, tn = 0;
+      for (int i = net * d.R; i < (net + 1) * d.R; ++i) { cn += st[2 * i]; tn += st[2 * i + 1]; }
+      printf("  net %d loop: %.0f cycles/step, %.3f us/step\n", net, cn / d.R / d.Tp, tn / d.R / 100.0 / d.Tp);
+    }
+    runf(gru_fwd_fused_kernel<6, 5>);
     CK(hipMemcpy(st.data(), w.slab_mix, st.size() * 8, hipMemcpyDeviceToHost));
     cyc = 0; for (int i = 0; i < 2 * d.R; ++i) cyc += st[2 * i];
     printf("fused fwd V4 stamped: %.0f cycles/step\n", cyc / (2 * d.R) / d.Tp);
     {
       CK(hipFree(w.slab_mix)); CK(hipMalloc(&w.slab_mix, 16 * 8 * 2 * d.R));
-      runf(gru_fwd_fused_kernel<64>);
+      runf(gru_fwd_fused_kernel<64, 5>);
       std::vector<uint64_t> sb(16 * 2 * d.R);
       CK(hipMemcpy(sb.data(), w.slab_mix, sb.size() * 8, hipMemcpyDeviceToHost));
       uint64_t t0 = ~0ull;
@@ -138,10 +178,14 @@ int main(int argc, char** argv) {
         printf("\n");
       }
     }
-    for (int var : {8, 12}) {
+    for (int var : {8, 12, 136, 264, 648, 1544}) {
       CK(hipFree(w.slab_mix)); CK(hipMalloc(&w.slab_mix, 16 * 8 * 2 * d.R));
-      if (var == 8) runf(gru_fwd_fused_kernel<8>);
-      else runf(gru_fwd_fused_kernel<12>);
+      if (var == 8) runf(gru_fwd_fused_kernel<8, 5>);
+      else if (var == 12) runf(gru_fwd_fused_kernel<12, 5>);
+      else if (var == 136) runf(gru_fwd_fused_kernel<136, 5>);
+      else if (var == 264) runf(gru_fwd_fused_kernel<264, 5>);
+      else if (var == 648) runf(gru_fwd_fused_kernel<648, 5>);
+      else runf(gru_fwd_fused_kernel<1544, 5>);
 
       std::vector<uint64_t> sb(16 * 2 * d.R);
       CK(hipMemcpy(sb.data(), w.slab_mix, sb.size() * 8, hipMemcpyDeviceToHost));
@@ -168,6 +212,16 @@ int main(int argc, char** argv) {
     };
     printf("fused bwd %.1f us\n", runbf(gru_bwd_fused_kernel<0>));
     printf("fused bwd V4(no producer MFMA) %.1f us\n", runbf(gru_bwd_fused_kernel<4>));
+    printf("fused bwd V128(chain prio) %.1f us\n", runbf(gru_bwd_fused_kernel<128>));
+    {
+      std::vector<float> a, b;
+      for (int round = 0; round < 9; ++round) {
+        a.push_back(runbf(gru_bwd_fused_kernel<0>));
+        b.push_back(runbf(gru_bwd_fused_kernel<128>));
+      }
+      std::sort(a.begin(), a.end()); std::sort(b.begin(), b.end());
+      printf("fused bwd V0 median %.1f min %.1f | V128 median %.1f min %.1f\n", a[4], a[0], b[4], b[0]);
+    }
     CK(hipFree(w.slab_mix)); CK(hipMalloc(&w.slab_mix, 32 * 8 * d.R));
     for (int var : {8, 12}) {
       if (var == 8) runbf(gru_bwd_fused_kernel<8>); else runbf(gru_bwd_fused_kernel<12>);
