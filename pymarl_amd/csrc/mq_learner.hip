@@ -231,8 +231,9 @@ struct RedBuilder {
     R.ng = (nslab + R.zc - 1) / R.zc;
     R.tmp = tmp;
     tmp += R.ng * len;
-    const int nb = (int)((len + 255) / 256);
-    R.blk1 = b1; b1 += nb * R.ng;
+    R.vec = (len % 4 == 0 && R.pitch % 4 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)R.tmp & 15) == 0) ? 1 : 0;
+    const int nb = (int)((len + 255) / 256), nb1 = R.vec ? (int)((len + 1023) / 1024) : nb;
+    R.blk1 = b1; b1 += nb1 * R.ng;
     R.blk2 = b2; b2 += nb;
   }
 };
