@@ -25,8 +25,11 @@ from collections import OrderedDict
 import numpy as np
 
 
-def make_replay(n_episodes, episode_limit, n_agents, n_actions, obs_dim, state_dim, seed=0, ragged=False):
-    """Return an OrderedDict of numpy arrays in the reference scheme layout (see module docstring)."""
+def make_replay(n_episodes, episode_limit, n_agents, n_actions, obs_dim, state_dim, seed=0, ragged=False,
+                min_len=None):
+    """Return an OrderedDict of numpy arrays in the reference scheme layout (see module docstring).
+
+    ragged: episode lengths uniform in [min_len, T] (min_len defaults to T // 2, the fixtures' recipe)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     N, T, n, A = int(n_episodes), int(episode_limit), int(n_agents), int(n_actions)
     Tp = T + 1
@@ -42,7 +45,7 @@ def make_replay(n_episodes, episode_limit, n_agents, n_actions, obs_dim, state_d
     filled = np.ones((N, Tp, 1), dtype=np.int64)
 
     if ragged:
-        lengths = rng.integers(max(1, T // 2), T + 1, size=N)
+        lengths = rng.integers(max(1, T // 2) if min_len is None else max(1, int(min_len)), T + 1, size=N)
     else:
         lengths = np.full(N, T, dtype=np.int64)
     for e in range(N):

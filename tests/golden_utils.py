@@ -55,6 +55,32 @@ class Case:
         return out
 
 
+class SynthCase(Case):
+    """A Case without a reference fixture: replay, weights and sampled ids from the same seeded generators, for
+    shapes the reference goldens do not cover (edge cases: checked against the oracle only, "parity unpinned"
+    against the reference itself; the oracle is pinned on the fixture shapes)."""
+
+    def __init__(self, name, n, A, O, S, T, B, n_episodes, steps, mixer="qmix", ragged=True, min_len=1,
+                 data_seed=11, weight_seed=12, sampler_seed=13):
+        self.name = name
+        self.n, self.A, self.O, self.S, self.T, self.B = n, A, O, S, T, B
+        self.n_episodes, self.steps, self.mixer, self.ragged = n_episodes, steps, mixer, ragged
+        self.episodes = [8 * k for k in range(steps)]
+        self.data = make_replay(n_episodes, T, n, A, O, S, seed=data_seed, ragged=ragged, min_len=min_len)
+        self.I = O + A + n
+        self.agent_shapes = agent_param_shapes(self.I, 64, A)
+        self.mixer_shapes = qmix_param_shapes(S, n, 32) if mixer == "qmix" else OrderedDict()
+        self.agent_params = init_params(self.agent_shapes, seed=weight_seed)
+        self.mixer_params = init_params(self.mixer_shapes, seed=weight_seed + 100) if mixer == "qmix" else OrderedDict()
+        self.sampler_seed = sampler_seed
+        state = np.random.get_state()   # the ids ReplayBuffer.sample draws after np.random.seed(sampler_seed)
+        np.random.seed(sampler_seed)
+        ids = [np.arange(B) if n_episodes == B else np.random.choice(n_episodes, B, replace=False)
+               for _ in range(steps)]
+        np.random.set_state(state)
+        self.z = {"ids": np.stack(ids)}
+
+
 def rel_err(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)

@@ -141,9 +141,14 @@ UNFUSED_ENV = ("MQ_UNFUSED_FWD", "MQ_UNFUSED_BWD", "MQ_GEMM_HYPER")
     # the A/B switches: the unfused kernel sequence on the shapes the fused kernels normally take
     ("cfg2_qmix", 4, True), ("cfg2_qmix_ragged", 3, True), ("tiny_vdn", 2, True)])
 def test_teacher_forced_steps(cases, name, steps, unfused, monkeypatch):
+    run_teacher_forced(get_case(cases, name), steps, unfused, monkeypatch)
+
+
+def run_teacher_forced(case, steps, unfused, monkeypatch):
+    """Every step from the oracle's state; decisions, stats, gradients and the RMSprop step checked (see module doc)."""
     from oracle.qlearner_np import OracleQLearner, fc1_preacts
     from tests.gpu_helpers import build, flat_grads, flat_params, rel
-    case = get_case(cases, name)
+    name = case.name
     for k in UNFUSED_ENV:   # read once, at handle creation (mq_create)
         if unfused:
             monkeypatch.setenv(k, "1")
