@@ -162,6 +162,51 @@ def build_coma_workload(cfg_name, device, n_episodes=1000, unique=128, seed=0, d
     return args, buf, learner, data, mac
 
 
+def rollout_baseline(cfg_name, device, budget_s=6.0):
+    """The rollout side (north_star: ParallelRunner stays on the host cores), timed on this host: EpisodeRunner on
+    the seeded FakeEnv at the config's shape (SC2 / SMAC cannot run offline), the HIP MAC step choosing actions,
+    episodes written straight into an HBM replay. One env process, batch_size_run = 1 (the episode runner)."""
+    import torch as th
+    from pymarl_amd.components.episode_buffer import ReplayBuffer
+    from pymarl_amd.components.transforms import OneHot
+    from pymarl_amd.controllers import REGISTRY as mac_REGISTRY
+    from pymarl_amd.runners import REGISTRY as r_REGISTRY
+    from pymarl_amd.utils.logging import Logger
+    _, n, A, O, S, T, B, _ = CONFIGS[cfg_name]
+    args = SN(n_agents=n, n_actions=A, state_shape=S, obs_shape=O, rnn_hidden_dim=64, obs_last_action=True,
+              obs_agent_id=True, agent="rnn", mac="basic_mac", agent_output_type="q",
+              action_selector="epsilon_greedy", epsilon_start=1.0, epsilon_finish=0.05, epsilon_anneal_time=50000,
+              batch_size_run=1, env="fake", env_args=dict(n_agents=n, n_actions=A, obs_dim=O, state_dim=S,
+                                                           episode_limit=T, seed=5),
+              device=str(device), use_cuda=True, test_nepisode=1, runner_log_interval=10 ** 9)
+    logger = Logger(logging.getLogger("bench-rollout"))
+    runner = r_REGISTRY["episode"](args, logger)
+    scheme = {"state": {"vshape": S}, "obs": {"vshape": O, "group": "agents"},
+              "actions": {"vshape": (1,), "group": "agents", "dtype": th.long},
+              "avail_actions": {"vshape": (A,), "group": "agents", "dtype": th.int},
+              "reward": {"vshape": (1,)}, "terminated": {"vshape": (1,), "dtype": th.uint8}}
+    groups = {"agents": n}
+    preprocess = {"actions": ("actions_onehot", [OneHot(out_dim=A)])}
+    buf = ReplayBuffer(scheme, groups, 256, T + 1, preprocess=preprocess, device=device)
+    mac = mac_REGISTRY["basic_mac"](buf.scheme, groups, args)
+    mac.cuda()
+    runner.setup(scheme=scheme, groups=groups, preprocess=preprocess, mac=mac)
+    buf.insert_episode_batch(runner.run(test_mode=False))   # warm-up episode
+    th.cuda.synchronize()
+    steps, eps, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        b = runner.run(test_mode=False)
+        buf.insert_episode_batch(b)
+        steps += int(b["filled"].sum().item()) - 1
+        eps += 1
+    th.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env steps/s", "cores": 1, "kind": "port",
+            "sample": f"{eps} EpisodeRunner episodes ({steps} env steps) on FakeEnv at {cfg_name}'s shape "
+                      f"(n={n}, A={A}, obs={O}, state={S}, limit={T}); SC2 unavailable offline; HIP MAC step, "
+                      f"HBM replay inserts; {dt / eps * 1e3:.1f} ms/episode"}
+
+
 def cpu_baseline(cfg_name, data, budget_s=12.0):
     """Time the numpy oracle's train() on this host's cores (bounded sample)."""
     from oracle.qlearner_np import OracleQLearner
@@ -426,9 +471,10 @@ def main():
                 "unit": "TFLOP/s", "frac": (achieved / FP32_PEAK_TFLOPS) if achieved else None,
                 "traffic": traffic, "launch_ms": dom_ms, "flops_per_launch": fl,
                 "fused": {"fwd": fused_fwd, "bwd": fused_bwd}}
-        cpu = None
+        cpu = rollout = None
         if world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(a.config, data)
+            rollout = rollout_baseline(a.config, device)
         bytes_per_sample = (O * 4 + (S * 4) / n + 8 + A * 4 + (4 + 1 + 8) / n)   # read-once replay bytes
         line = {
             "metric": METRIC, "value": value, "unit": "samples/s", "n_gpus": world, "steps": a.steps,
@@ -441,6 +487,7 @@ def main():
             "hbm_roofline_whole_step": {"achieved_GBs": value * bytes_per_sample / 1e9, "peak_GBs": HBM_PEAK_GBS,
                                         "frac": value * bytes_per_sample / 1e9 / HBM_PEAK_GBS},
             "cpu_baseline": cpu,
+            "rollout_baseline": rollout,
         }
         print(json.dumps(line))
     if world > 1:
