@@ -19,6 +19,7 @@
 //
 // MFMA maps as gru_fwd_fused.hpp (v_mfma_f32_16x16x4_f32: A[i = c][kk = g], B[kk = g][j = c], D[4g + r][c]).
 #pragma once
+#include <cstdlib>
 #include "gru_fwd_fused.hpp"
 
 namespace mq {
@@ -37,8 +38,8 @@ struct BwdFusedLds {
 
 inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_fwd_ok(I, O, A, n, RT); }
 
-// VAR: ablation bits for scripts/rec_micro.hip only (production = 0): 4 producers do no MFMA work, 8 per-phase
-// cycle bins of the chain.
+// VAR: ablation bits (production = 0): 4 producers do no MFMA work, 8 per-phase cycle bins of the chain
+// (scripts/rec_micro.hip), 128 chain waves at s_setprio 2, 256 the chain's inputs loaded two steps ahead.
 template <int VAR = 0>
 __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
                                                             Work w, int64_t slab_len, int64_t slab1_len) {
@@ -119,8 +120,10 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     const float m0 = q == 0 ? 1.0f : 0.0f, m1 = q == 1 ? 1.0f : 0.0f, m2 = q == 2 ? 1.0f : 0.0f;
     const float m3 = q == 3 ? 1.0f : 0.0f;
     float carry = 0.0f, db_i = 0.0f, db_h = 0.0f;   // bias grads: this lane's component q of b_ih / b_hh
-    auto step = [&](int t, const In& cur, In& nxt) {
-      load(t - 1, nxt);   // previous (earlier) step's inputs, in flight under this step
+    // ahead: the slot whose loads are issued this step (t - 1 with two slots; t - 2 with three, VAR 256, so every
+    // load has two chain steps of latency instead of one); nxt: the next step's slot, whose w2 is looked up here
+    auto step = [&](int t, const In& cur, In& nxt, In& ahead, int dist) {
+      load(t - dist, ahead);
       const int p = t & (FCH - 1), cb = (t / FCH) & 1;
       const float gr = quad_bcast<0>(cur.g), gz = quad_bcast<1>(cur.g), gn = quad_bcast<2>(cur.g),
                   ghn = quad_bcast<3>(cur.g);
@@ -153,8 +156,9 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       carry = cz + quad_sum((a01.x + a01.y) + (a23.x + a23.y));
       lookup_w2(nxt);
     };
-    In sa, sb;
+    In sa, sb, sc;
     load(Tp - 1, sa);
+    if (VAR & 256) load(Tp - 2, sb);
     drain_vmem();
     lds_barrier();
     lookup_w2(sa);
@@ -167,9 +171,9 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       const uint64_t c0 = __builtin_amdgcn_s_memtime();
       for (; t >= 0; t -= 2) {
         const uint64_t a0 = __builtin_amdgcn_s_memtime();
-        step(t, sa, sb);
+        step(t, sa, sb, sb, 1);
         const uint64_t a1 = __builtin_amdgcn_s_memtime();
-        if (t - 1 >= 0) step(t - 1, sb, sa);
+        if (t - 1 >= 0) step(t - 1, sb, sa, sa, 1);
         const uint64_t a2 = __builtin_amdgcn_s_memtime();
 #pragma unroll
         for (int i = 0; i < FCH; ++i) {
@@ -183,12 +187,20 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
         for (int i = 0; i < FCH; ++i) st[i] = bins[i];
         st[16] = __builtin_amdgcn_s_memtime() - c0;
       }
+    } else if (VAR & 256) {
+      for (; t - 2 >= 0; t -= 3) {
+        step(t, sa, sb, sc, 2);
+        step(t - 1, sb, sc, sa, 2);
+        step(t - 2, sc, sa, sb, 2);
+      }
+      if (t >= 0) step(t, sa, sb, sc, 2);
+      if (t - 1 >= 0) step(t - 1, sb, sc, sa, 2);
     } else {
       for (; t - 1 >= 0; t -= 2) {
-        step(t, sa, sb);
-        step(t - 1, sb, sa);
+        step(t, sa, sb, sb, 1);
+        step(t - 1, sb, sa, sa, 1);
       }
-      if (t >= 0) step(t, sa, sb);
+      if (t >= 0) step(t, sa, sb, sb, 1);
     }
     if (VAR & 128) __builtin_amdgcn_s_setprio(0);
     lds_barrier();   // producer tail: chunk 0 (2 barriers)
@@ -385,6 +397,21 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
   if (tid < H)
     w.slab_fc1[(int64_t)blockIdx.x * slab1_len + H * I + tid] =
         (S.db1[0][tid] + S.db1[1][tid]) + (S.db1[2][tid] + S.db1[3][tid]);
+}
+
+// Host: production is VAR 256 (inputs two steps ahead: -2.5 us in the cfg2 pipeline, r01k A/B); MQ_BWD_VAR
+// selects another variant for in-pipeline A/B runs.
+inline void launch_bwd_fused(dim3 grid, size_t dyn, hipStream_t s, const Dims& d, const Rep& rp, const float* P,
+                             const Lay& L, const Work& w, int64_t slab_len, int64_t slab1_len) {
+  static const int var = [] { const char* e = std::getenv("MQ_BWD_VAR"); return e ? std::atoi(e) : 256; }();
+  if (var == 256)
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<256>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else if (var == 128)
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<128>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else if (var == 384)
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<384>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<0>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
 }
 
 }  // namespace mq

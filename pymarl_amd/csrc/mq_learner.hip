@@ -437,8 +437,7 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
     h->nblk_bwd = d.R;
     h->nsplit_fc1 = d.R;
     const size_t dyn = ((size_t)2 * d.A * mq::H + d.A) * sizeof(float);
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<0>, dim3(d.R), dim3(512), dyn, s, d, rp, (const float*)h->on, L, w,
-                       h->len_rnn, (int64_t)mq::H * d.I + mq::H);
+    launch_bwd_fused(dim3(d.R), dyn, s, d, rp, (const float*)h->on, L, w, h->len_rnn, (int64_t)mq::H * d.I + mq::H);
     MQ_HIP(hipGetLastError());
   } else {
     {
