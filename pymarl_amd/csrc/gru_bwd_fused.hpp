@@ -39,7 +39,8 @@ struct BwdFusedLds {
 inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_fwd_ok(I, O, A, n, RT); }
 
 // VAR: ablation bits (production = 0): 4 producers do no MFMA work, 8 per-phase cycle bins of the chain
-// (scripts/rec_micro.hip), 128 chain waves at s_setprio 2, 256 the chain's inputs loaded two steps ahead.
+// (scripts/rec_micro.hip), 128 chain waves at s_setprio 2, 256 the chain's inputs loaded two steps ahead,
+// 512 the X1 / XIN rows of the next chunk loaded one chunk ahead.
 template <int VAR = 0>
 __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
                                                             Work w, int64_t slab_len, int64_t slab1_len) {
@@ -335,6 +336,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     for (int c = cl; c >= 0; --c) {
       const int C = c + 1;
       const bool work = !(VAR & 4) && C <= cl;
+      if ((VAR & 512) && c == cl) issue_rows(cl);   // VAR 512: rows one chunk ahead (the top chunk's up front)
 #pragma unroll
       for (int u = 0; u < FCH; ++u) {
         const int t = FCH * c + FCH - 1 - u;
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
         lds_barrier();   // step t's records published
         fc2_grads(t);
         if (work) {
-          if (u == 0) issue_rows(C);
+          if (u == 0 && !(VAR & 512)) issue_rows(C);
           if (u >= 1 && u <= 4) dw_rec(C, u - 1, u, false);
           if (u == 4) store_rows(C);
           if (u >= 5 && u <= 8) dw_rec(C, u - 5, u - 4, true);
@@ -352,11 +354,12 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
           if (u == 14) dw1_part(1, 2);
           if (u == 15) dw1_part(2, 4);
         }
+        if ((VAR & 512) && u == 5 && c < cl) issue_rows(c);   // stored at u = 4 of the next chunk
       }
     }
     // tail: chunk 0 (2 barriers, matched by the chain waves)
     if (!(VAR & 4)) {
-      issue_rows(0);
+      if (!(VAR & 512)) issue_rows(0);
       dw_rec(0, 0, 4, false);
       drain_vmem();
       store_rows(0);
@@ -399,15 +402,18 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
         (S.db1[0][tid] + S.db1[1][tid]) + (S.db1[2][tid] + S.db1[3][tid]);
 }
 
-// Host: production is VAR 256 (inputs two steps ahead: -2.5 us in the cfg2 pipeline, r01k A/B); MQ_BWD_VAR
+// Host: production is VAR 768 = 256 (chain inputs two steps ahead: -2.5 us in the cfg2 pipeline, r01k A/B) + 512
+// (X1 / XIN rows one chunk ahead: -0.7 us); MQ_BWD_VAR
 // selects another variant for in-pipeline A/B runs.
 inline void launch_bwd_fused(dim3 grid, size_t dyn, hipStream_t s, const Dims& d, const Rep& rp, const float* P,
                              const Lay& L, const Work& w, int64_t slab_len, int64_t slab1_len) {
-  static const int var = [] { const char* e = std::getenv("MQ_BWD_VAR"); return e ? std::atoi(e) : 256; }();
+  static const int var = [] { const char* e = std::getenv("MQ_BWD_VAR"); return e ? std::atoi(e) : 768; }();
   if (var == 256)
     hipLaunchKernelGGL(gru_bwd_fused_kernel<256>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
   else if (var == 128)
     hipLaunchKernelGGL(gru_bwd_fused_kernel<128>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else if (var == 768)
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
   else if (var == 384)
     hipLaunchKernelGGL(gru_bwd_fused_kernel<384>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
   else
