@@ -105,8 +105,17 @@ int main(int argc, char** argv) {
       return time_it([&] { hipLaunchKernelGGL(kern, dim3(d.R, 2), dim3(512), 0, 0, d, rf, (const float*)P0, (const float*)P1, L, w); });
     };
     printf("fused fwd %.1f us\n", runf(gru_fwd_fused_kernel<0, 5>));
+    {
+      auto run1 = [&]() {
+        return time_it([&] { hipLaunchKernelGGL((gru_fwd_fused_kernel<0, 5>), dim3(d.R, 1), dim3(512), 0, 0, d, rf, (const float*)P0, (const float*)P1, L, w); });
+      };
+      std::vector<float> a, b;
+      for (int round = 0; round < 7; ++round) { a.push_back(runf(gru_fwd_fused_kernel<0, 5>)); b.push_back(run1()); }
+      std::sort(a.begin(), a.end()); std::sort(b.begin(), b.end());
+      printf("fused fwd both nets median %.1f us | online net only (grid R x 1) median %.1f us\n", a[3], b[3]);
+    }
     {  // interleaved rounds (one process): median / min per variant
-      const char* names[] = {"V0", "V128 prio", "V512 rebal", "V640 prio+rebal", "V1536 tprio+rebal"};
+      const char* names[] = {"V0 (prio)", "V128 no prio", "V512 rebal", "V640 rebal no prio", "V1536 tprio+rebal"};
       std::vector<std::vector<float>> ts(5);
       for (int round = 0; round < 9; ++round) {
         ts[0].push_back(runf(gru_fwd_fused_kernel<0, 5>));
@@ -123,10 +132,10 @@ int main(int argc, char** argv) {
     printf("fused fwd V1(no Hs/Gates st) %.1f us\n", runf(gru_fwd_fused_kernel<1, 5>));
     printf("fused fwd V4(no chunk pipeline) %.1f us\n", runf(gru_fwd_fused_kernel<4, 5>));
     printf("fused fwd V5 %.1f us\n", runf(gru_fwd_fused_kernel<5, 5>));
-    printf("fused fwd V128(chain prio) %.1f us\n", runf(gru_fwd_fused_kernel<128, 5>));
+    printf("fused fwd V128(no chain prio) %.1f us\n", runf(gru_fwd_fused_kernel<128, 5>));
     printf("fused fwd V256(early gather) %.1f us\n", runf(gru_fwd_fused_kernel<256, 5>));
-    printf("fused fwd V384(both) %.1f us\n", runf(gru_fwd_fused_kernel<384, 5>));
-    printf("fused fwd V640(prio+rebalanced) %.1f us\n", runf(gru_fwd_fused_kernel<640, 5>));
+    printf("fused fwd V384(early gather, no prio) %.1f us\n", runf(gru_fwd_fused_kernel<384, 5>));
+    printf("fused fwd V640(rebalanced, no prio) %.1f us\n", runf(gru_fwd_fused_kernel<640, 5>));
     printf("fused fwd V512(rebalanced) %.1f us\n", runf(gru_fwd_fused_kernel<512, 5>));
     printf("fused fwd V1536(target prio+rebalanced) %.1f us\n", runf(gru_fwd_fused_kernel<1536, 5>));
     printf("fused fwd V1280(target prio+early) %.1f us\n", runf(gru_fwd_fused_kernel<1280, 5>));
