@@ -487,14 +487,13 @@ inline void launch_fwd_fused_v(dim3 grid, hipStream_t s, const Dims& d, const Re
     hipLaunchKernelGGL((gru_fwd_fused_kernel<VAR, FGATHER>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
 }
 // MQ_FWD_VAR (A/B runs of the schedule variants in the real pipeline, where the obs gather reads cold HBM):
-// 256 gathers two chunks ahead, 512 the rebalanced schedule. Unset = production.
+// 128 chains without priority, 256 gathers two chunks ahead, 512 the rebalanced schedule. Unset = production. Only
+// result-preserving variants are reachable here; the diagnostic bits (no loads / no stores) stay in rec_micro.
 inline void launch_fwd_fused(dim3 grid, hipStream_t s, const Dims& d, const Rep& rp, const float* P0, const float* P1,
                              const Lay& L, const Work& w) {
   static const int var = [] { const char* e = std::getenv("MQ_FWD_VAR"); return e ? std::atoi(e) : 0; }();
   if (var == 256) launch_fwd_fused_v<256>(grid, s, d, rp, P0, P1, L, w);
   else if (var == 512) launch_fwd_fused_v<512>(grid, s, d, rp, P0, P1, L, w);
-  else if (var == 16) launch_fwd_fused_v<16>(grid, s, d, rp, P0, P1, L, w);    // diagnostic: no obs loads
-  else if (var == 32) launch_fwd_fused_v<32>(grid, s, d, rp, P0, P1, L, w);    // diagnostic: no X1 / XIN stores
   else if (var == 128) launch_fwd_fused_v<128>(grid, s, d, rp, P0, P1, L, w);  // no chain priority
   else launch_fwd_fused_v<0>(grid, s, d, rp, P0, P1, L, w);
 }
