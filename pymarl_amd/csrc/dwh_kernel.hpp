@@ -11,20 +11,25 @@
 // waves take interleaved quarters of that slice and are summed through LDS, so each workgroup writes one partial
 // tile (coalesced along s) into slab[z] in the parameter layout relative to hyper_w_1.weight. red_pass1 sums the
 // nsplit partials. The m loop is branch-free: rows past the slice read a clamped row with a zero factor.
+//
+// Two instances: dwh_kernel (8 MFMAs per pipelined block, serial after the BPTT) and dwh_side_kernel (2 per block,
+// capped at 48 VGPRs by __launch_bounds__(256, 10); the compiler's warning that LDS holds its occupancy at 6 is
+// expected), which runs on a second stream beside the fused BPTT: the BPTT workgroup (one per CU, 231 -> 232 VGPRs
+// x 2 waves per SIMD, 134 KB + W2 of LDS) leaves 48 VGPRs per SIMD and ~22 KB of LDS free, room for one dwh_side
+// workgroup (17 KB).
+// Each wave walks the same m steps in the same order in both, so their results are bitwise equal.
 #pragma once
 #include "learner_gemms.hpp"
 
 namespace mq {
 
 constexpr int DWH_T = 32;   // output tile edge
-constexpr int DWH_U = 8;    // MFMAs (2 m-rows each) per pipelined block
 
 // grid = ceil(NH / 32) * ceil((S + 1) / 32) * nsplit (tiles_j = ceil(NH / 32)), 256 threads.
-// VAR (scripts/rec_micro.hip only): 1 no MFMA, 2 no operand loads.
-template <int VAR = 0>
-__global__ __launch_bounds__(256) void dwh_kernel(Dims d, Lay L, const float* __restrict__ dHYP,
-                                                  const float* __restrict__ S0, float* __restrict__ slab,
-                                                  int64_t len, int nsplit, int tiles_j) {
+// VAR (scripts/rec_micro.hip only): 1 no MFMA, 2 no operand loads. U: MFMAs (2 m-rows each) per pipelined block.
+template <int VAR, int U>
+MQ_DEV void dwh_body(const Dims& d, const Lay& L, const float* __restrict__ dHYP, const float* __restrict__ S0,
+                     float* __restrict__ slab, int64_t len, int nsplit, int tiles_j) {
   __shared__ float red[4][DWH_T * (DWH_T + 1)];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int NH = d.NH, S = d.S, M = d.M;
@@ -41,10 +46,10 @@ __global__ __launch_bounds__(256) void dwh_kernel(Dims d, Lay L, const float* __
   const float amul = s < S ? 1.0f : 0.0f, aadd = s == S ? 1.0f : 0.0f;
 
   f32x16 acc = {};
-  float a0[DWH_U], b0[DWH_U], a1[DWH_U], b1[DWH_U];   // two register buffers (static indices only)
-  auto load = [&](float (&a)[DWH_U], float (&b)[DWH_U], int st0) {
+  float a0[U], b0[U], a1[U], b1[U];   // two register buffers (static indices only)
+  auto load = [&](float (&a)[U], float (&b)[U], int st0) {
 #pragma unroll
-    for (int u = 0; u < DWH_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int stp = st0 + 4 * u;
       const int m = 2 * stp + half;
       const int mc = min(m, M - 1);
@@ -57,14 +62,14 @@ __global__ __launch_bounds__(256) void dwh_kernel(Dims d, Lay L, const float* __
       }
     }
   };
-  auto mma = [&](const float (&a)[DWH_U], const float (&b)[DWH_U]) {
+  auto mma = [&](const float (&a)[U], const float (&b)[U]) {
 #pragma unroll
-    for (int u = 0; u < DWH_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       if (VAR & 1) acc[u] = fmaf(a[u], b[u], acc[u]);
       else acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
     }
   };
-  constexpr int BLK = 4 * DWH_U;   // steps per block over the four waves
+  constexpr int BLK = 4 * U;   // steps per block over the four waves
   int st = sb + wv;
   const int nblk = (se - sb + BLK - 1) / BLK;
   if (nblk > 0) load(a0, b0, st);
@@ -93,6 +98,19 @@ __global__ __launch_bounds__(256) void dwh_kernel(Dims d, Lay L, const float* __
       else out[sg.b - base + sg.row] = v;
     }
   }
+}
+
+template <int VAR = 0>
+__global__ __launch_bounds__(256) void dwh_kernel(Dims d, Lay L, const float* __restrict__ dHYP,
+                                                  const float* __restrict__ S0, float* __restrict__ slab,
+                                                  int64_t len, int nsplit, int tiles_j) {
+  dwh_body<VAR, 8>(d, L, dHYP, S0, slab, len, nsplit, tiles_j);
+}
+
+__global__ __launch_bounds__(256, 10) void dwh_side_kernel(
+    Dims d, Lay L, const float* __restrict__ dHYP, const float* __restrict__ S0, float* __restrict__ slab, int64_t len,
+    int nsplit, int tiles_j) {
+  dwh_body<0, 2>(d, L, dHYP, S0, slab, len, nsplit, tiles_j);
 }
 
 }  // namespace mq

@@ -88,6 +88,10 @@ struct mq_handle {
   int dwh_split = getenv("MQ_DWH_SPLIT") ? atoi(getenv("MQ_DWH_SPLIT")) : 8;   // m-slices of the dW_hyper pass
   bool generic_mix = getenv("MQ_GENERIC_MIX") != nullptr;   // A/B switch: mix_kernel instead of mix_fast_kernel
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
+  // dW_hyper on a side stream beside the fused BPTT (dwh_kernel.hpp); MQ_DWH_OVERLAP=0 keeps it in stream order
+  bool dwh_overlap = !getenv("MQ_DWH_OVERLAP") || atoi(getenv("MQ_DWH_OVERLAP")) != 0;
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
   int slots = 0;
   uint32_t mask = 0;
@@ -238,6 +242,32 @@ struct RedBuilder {
   }
 };
 
+// Side stream and fork / join events of the dW_hyper overlap, created on first use. Lowest stream priority: the
+// BPTT on the caller's stream keeps the arbiter's preference.
+hipError_t ensure_side(mq_handle* h) {
+  if (h->side) return hipSuccess;
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, least);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
+  return e;
+}
+
+// dW_hyper: 32 x 32 output tiles x nsplit m-slices, operands straight from global memory (dwh_kernel.hpp)
+hipError_t launch_dwh(mq_handle* h, const Dims& d, const Lay& L, const Work& w, hipStream_t s, bool side) {
+  const int tj = (d.NH + DWH_T - 1) / DWH_T, ts = (d.S + 1 + DWH_T - 1) / DWH_T;
+  const int ns = std::max(1, std::min({h->dwh_split, kNsplitMax, (d.M + 1) / 2}));
+  h->nsplit_mix = ns;
+  if (side)
+    hipLaunchKernelGGL(dwh_side_kernel, dim3(tj * ts * ns), dim3(256), 0, s, d, L, (const float*)w.dHYP,
+                       (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj);
+  else
+    hipLaunchKernelGGL(dwh_kernel<0>, dim3(tj * ts * ns), dim3(256), 0, s, d, L, (const float*)w.dHYP,
+                       (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
@@ -331,6 +361,9 @@ int mq_destroy(mq_handle* h) {
   if (!h) return MQ_OK;
   for (auto e : h->ev0) (void)hipEventDestroy(e);
   for (auto e : h->ev1) (void)hipEventDestroy(e);
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  if (h->side) (void)hipStreamDestroy(h->side);
   if (h->ws) (void)hipFree(h->ws);
   delete h;
   return MQ_OK;
@@ -430,9 +463,27 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
                          (const float*)h->tg, L, w, curmax);
     MQ_HIP(hipGetLastError());
   }
-  pt.begin(PH_GRUB);
   const int rw_bwd = std::min(2, pick_rw(d.R, 256));
-  if (rw_bwd == 1 && fused_bwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused_bwd) {
+  const bool fused_bwd = rw_bwd == 1 && fused_bwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused_bwd;
+  // dW_hyper needs only the mixer's dHYP: forked onto the side stream it runs in the room the fused BPTT leaves on
+  // each CU, joined before the reduction (same arithmetic in the same order: bitwise the in-order result)
+  const bool side = fused_bwd && c.mixer == MQ_MIXER_QMIX && !h->force_unfused_mix && h->dwh_overlap;
+  if (side) {
+    MQ_HIP(ensure_side(h));
+    MQ_HIP(hipEventRecord(h->ev_fork, s));
+    MQ_HIP(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    const bool timed = h->slots > 0 && ((h->mask >> PH_DWH) & 1u);
+    const int ti = (int)(h->tstep % std::max(h->slots, 1)) * PH_N + PH_DWH;
+    if (timed) {
+      MQ_HIP(hipEventRecord(h->ev0[ti], h->side));
+      h->ev_used[ti] = 1;
+    }
+    MQ_HIP(launch_dwh(h, d, L, w, h->side, true));
+    if (timed) MQ_HIP(hipEventRecord(h->ev1[ti], h->side));
+    MQ_HIP(hipEventRecord(h->ev_join, h->side));
+  }
+  pt.begin(PH_GRUB);
+  if (fused_bwd) {
     // one row per workgroup: dW_hh / dW_ih / dX1 / dW1 on the chain's idle matrix cores (gru_bwd_fused.hpp)
     h->nblk_bwd = d.R;
     h->nsplit_fc1 = d.R;
@@ -465,16 +516,10 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
       MQ_HIP(launch_gemm(p, mq::H, d.I, ns, s));
     }
   }
-  if (c.mixer == MQ_MIXER_QMIX) {
+  if (c.mixer == MQ_MIXER_QMIX && !side) {
     pt.begin(PH_DWH);
     if (!h->force_unfused_mix) {
-      // 32 x 32 output tiles x nsplit m-slices, operands straight from global memory (dwh_kernel.hpp)
-      const int tj = (d.NH + DWH_T - 1) / DWH_T, ts = (d.S + 1 + DWH_T - 1) / DWH_T;
-      const int ns = std::max(1, std::min({h->dwh_split, kNsplitMax, (d.M + 1) / 2}));
-      h->nsplit_mix = ns;
-      hipLaunchKernelGGL(dwh_kernel<0>, dim3(tj * ts * ns), dim3(256), 0, s, d, L, (const float*)w.dHYP,
-                         (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj);
-      MQ_HIP(hipGetLastError());
+      MQ_HIP(launch_dwh(h, d, L, w, s, false));
     } else {
     const int tiles = ((d.NH + GBM - 1) / GBM) * ((d.S + DwhProb::BN - 1) / DwhProb::BN);
     int ns = std::max(1, std::min(kNsplitMax, std::min((512 + tiles - 1) / tiles, d.M / 64)));
@@ -484,6 +529,10 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
     DwhProb p{d, L, w.dHYP, w.S0, w.slab_mix, h->len_mix, ns};
     MQ_HIP(launch_gemm(p, d.NH, d.S, ns, s));
     }
+  }
+  if (side) {   // join: the reduction reads dW_hyper's slabs
+    pt.end();
+    MQ_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
   }
   pt.begin(PH_RED);
   {

@@ -118,6 +118,12 @@ __global__ __launch_bounds__(256) void apply_kernel(float* __restrict__ p, float
                                                     int64_t n, const float* __restrict__ part, int npart,
                                                     OptHP hp, float* __restrict__ stats) {
   __shared__ float sh[2];
+  // the first element's operands and the mask sum do not depend on the norm: their loads go out before it
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x, stride = (int64_t)gridDim.x * 256;
+  const bool have0 = i0 < n;
+  const float g0 = have0 ? g[i0] : 0.0f, v0 = have0 ? sq[i0] : 0.0f, p0 = have0 ? p[i0] : 0.0f;
+  const float* sums = g + n;   // MQ_NSUMS tail
+  const float msum = sums[1];
   if (threadIdx.x < 64) {
     float s = 0.0f;
     for (int i = threadIdx.x; i < npart; i += 64) s += part[i];
@@ -125,18 +131,18 @@ __global__ __launch_bounds__(256) void apply_kernel(float* __restrict__ p, float
     if (threadIdx.x == 0) sh[0] = s;
   }
   __syncthreads();
-  const float* sums = g + n;   // MQ_NSUMS tail
-  const float msum = sums[1];
   const float inv = 1.0f / msum;
   const float norm = sqrtf(sh[0]) * inv;
   const float coef = fminf(hp.clip / (norm + 1e-6f), 1.0f);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const float gi = (g[i] * inv) * coef;
+  auto upd = [&](int64_t i, float gv, float sv, float pv) {
+    const float gi = (gv * inv) * coef;
     g[i] = gi;
-    const float v = sq[i] * hp.alpha + (1.0f - hp.alpha) * (gi * gi);
+    const float v = sv * hp.alpha + (1.0f - hp.alpha) * (gi * gi);
     sq[i] = v;
-    p[i] = p[i] + (-hp.lr) * (gi / (sqrtf(v) + hp.eps));
-  }
+    p[i] = pv + (-hp.lr) * (gi / (sqrtf(v) + hp.eps));
+  };
+  if (have0) upd(i0, g0, v0, p0);
+  for (int64_t i = i0 + stride; i < n; i += stride) upd(i, g[i], sq[i], p[i]);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     stats[0] = sums[0] / msum;                         // loss
     stats[1] = norm;                                   // grad_norm
