@@ -88,8 +88,9 @@ struct mq_handle {
   int dwh_split = getenv("MQ_DWH_SPLIT") ? atoi(getenv("MQ_DWH_SPLIT")) : 8;   // m-slices of the dW_hyper pass
   bool generic_mix = getenv("MQ_GENERIC_MIX") != nullptr;   // A/B switch: mix_kernel instead of mix_fast_kernel
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
-  // dW_hyper on a side stream beside the fused BPTT (dwh_kernel.hpp); MQ_DWH_OVERLAP=0 keeps it in stream order
-  bool dwh_overlap = !getenv("MQ_DWH_OVERLAP") || atoi(getenv("MQ_DWH_OVERLAP")) != 0;
+  // A/B switch, off by default: dW_hyper on a side stream beside the fused BPTT (dwh_kernel.hpp). Measured at cfg2
+  // (r01l): the co-resident dwh_side waves slow the BPTT chain 92.7 -> 105.6 us, the step 238 -> 264 us
+  bool dwh_overlap = getenv("MQ_DWH_OVERLAP") && atoi(getenv("MQ_DWH_OVERLAP")) != 0;
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
