@@ -16,7 +16,8 @@
 // capped at 48 VGPRs by __launch_bounds__(256, 10); the compiler's warning that LDS holds its occupancy at 6 is
 // expected), which runs on a second stream beside the fused BPTT: the BPTT workgroup (one per CU, 231 -> 232 VGPRs
 // x 2 waves per SIMD, 134 KB + W2 of LDS) leaves 48 VGPRs per SIMD and ~22 KB of LDS free, room for one dwh_side
-// workgroup (17 KB).
+// workgroup (17 KB). It fits, and loses: its MFMA waves on the chain's SIMDs slow the BPTT chain by 14 % (cfg2:
+// 92.7 -> 105.6 us, step 238 -> 264 us, r01l A/B), so it is an A/B switch only (MQ_DWH_OVERLAP=1).
 // Each wave walks the same m steps in the same order in both, so their results are bitwise equal.
 #pragma once
 #include "learner_gemms.hpp"
@@ -28,7 +29,7 @@ constexpr int DWH_T = 32;   // output tile edge
 // grid = ceil(NH / 32) * ceil((S + 1) / 32) * nsplit (tiles_j = ceil(NH / 32)), 256 threads.
 // VAR (scripts/rec_micro.hip only): 1 no MFMA, 2 no operand loads. U: MFMAs (2 m-rows each) per pipelined block.
 template <int VAR, int U>
-MQ_DEV void dwh_body(const Dims& d, const Lay& L, const float* __restrict__ dHYP, const float* __restrict__ S0,
+MQ_DEV void dwh_body(Dims d, Lay L, const float* __restrict__ dHYP, const float* __restrict__ S0,
                      float* __restrict__ slab, int64_t len, int nsplit, int tiles_j) {
   __shared__ float red[4][DWH_T * (DWH_T + 1)];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of dW_hyper on the side stream beside the fused BPTT (default) vs in stream order (MQ_DWH_OVERLAP=0), cfg2,
+# A/B of dW_hyper on the side stream beside the fused BPTT (MQ_DWH_OVERLAP=1) vs in stream order (default), cfg2,
 # interleaved rounds.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out

@@ -237,7 +237,7 @@ def test_fast_mix_kernel_bitwise(cases, name, monkeypatch):
 
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_qmix_ragged", "tiny_qmix"])
 def test_dwh_side_stream_bitwise(cases, name, monkeypatch):
-    """dW_hyper on the side stream beside the fused BPTT (default) equals the in-order launch bit for bit."""
+    """dW_hyper on the side stream beside the fused BPTT (MQ_DWH_OVERLAP=1) equals the in-order launch bit for bit."""
     from tests.gpu_helpers import build, flat_grads, flat_params
     case = get_case(cases, name)
     outs = []
