@@ -237,6 +237,8 @@ struct RedBuilder {
     R.tmp = tmp;
     tmp += R.ng * len;
     R.vec = (len % 4 == 0 && R.pitch % 4 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)R.tmp & 15) == 0) ? 1 : 0;
+    static const bool xcd_on = !getenv("MQ_RED_XCD") || atoi(getenv("MQ_RED_XCD")) != 0;   // A/B switch
+    R.xcd = (xcd_on && nslab % 128 == 0 && R.ng == kRedZ && b1 % 16 == 0) ? 1 : 0;
     const int nb = (int)((len + 255) / 256), nb1 = R.vec ? (int)((len + 1023) / 1024) : nb;
     R.blk1 = b1; b1 += nb1 * R.ng;
     R.blk2 = b2; b2 += nb;

@@ -23,6 +23,9 @@ struct RedRegion {
   int64_t pitch;    // slab stride in src (>= len: a region may cover a prefix of each slab)
   int nslab, zc, ng, sq;
   int vec;          // pass 1 in float4 (len, pitch multiples of 4; src and tmp 16-byte aligned)
+  int xcd;          // pass 1 groups slabs by XCD (ng = 16, nslab % 128 == 0, blk1 % 16 == 0): group g holds slabs
+                    // r == g (mod 8), summed by blocks with blockIdx == g (mod 8), i.e. on the XCD whose L2 holds
+                    // them when slab r was written by workgroup r (the per-row BPTT slabs)
   int blk1, blk2;   // first block of this region in pass 1 / pass 2
 };
 struct RedPlan {
@@ -42,31 +45,37 @@ __global__ __launch_bounds__(256) void red_pass1_kernel(RedPlan pl) {
   const int k = red_region(pl, blockIdx.x, false);
   const RedRegion& R = pl.r[k];
   if (R.vec) {   // 1024 elements per block, one float4 per thread and slab
-    const int nb = (int)((R.len + 1023) / 1024), lb = blockIdx.x - R.blk1, g = lb / nb, chunk = lb - g * nb;
+    const int nb = (int)((R.len + 1023) / 1024), lb = blockIdx.x - R.blk1;
+    const int g = R.xcd ? lb % R.ng : lb / nb, chunk = R.xcd ? lb / R.ng : lb - g * nb;
     const int64_t i = (int64_t)chunk * 1024 + 4 * threadIdx.x;
     if (i >= R.len) return;
     const int z0 = g * R.zc, z1 = min(R.nslab, z0 + R.zc);
+    // slab of group member z: z itself, or (XCD grouping) the (z - z0)-th slab r == g (mod 8) of sub-group g / 8
+    auto slab = [&](int z) { return R.xcd ? 8 * ((g >> 3) * R.zc + (z - z0)) + (g & 7) : z; };
     f32x4 v[kRedZ];
     f32x4 s = {0.0f, 0.0f, 0.0f, 0.0f};
     for (int zb = z0; zb < z1; zb += kRedZ) {
 #pragma unroll
       for (int u = 0; u < kRedZ; ++u)
-        v[u] = (zb + u < z1) ? *(const f32x4*)(R.src + (int64_t)(zb + u) * R.pitch + i) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        v[u] = (zb + u < z1) ? *(const f32x4*)(R.src + (int64_t)slab(zb + u) * R.pitch + i)
+                             : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int u = 0; u < kRedZ; ++u) s += v[u];   // per component: the scalar path's order
     }
     *(f32x4*)(R.tmp + (int64_t)g * R.len + i) = s;
     return;
   }
-  const int nb = (int)((R.len + 255) / 256), lb = blockIdx.x - R.blk1, g = lb / nb, chunk = lb - g * nb;
+  const int nb = (int)((R.len + 255) / 256), lb = blockIdx.x - R.blk1;
+  const int g = R.xcd ? lb % R.ng : lb / nb, chunk = R.xcd ? lb / R.ng : lb - g * nb;
   const int64_t i = (int64_t)chunk * 256 + threadIdx.x;
   if (i >= R.len) return;
   const int z0 = g * R.zc, z1 = min(R.nslab, z0 + R.zc);
+  auto slab = [&](int z) { return R.xcd ? 8 * ((g >> 3) * R.zc + (z - z0)) + (g & 7) : z; };
   float v[kRedZ];
   float s = 0.0f;
   for (int zb = z0; zb < z1; zb += kRedZ) {
 #pragma unroll
-    for (int u = 0; u < kRedZ; ++u) v[u] = (zb + u < z1) ? R.src[(int64_t)(zb + u) * R.pitch + i] : 0.0f;
+    for (int u = 0; u < kRedZ; ++u) v[u] = (zb + u < z1) ? R.src[(int64_t)slab(zb + u) * R.pitch + i] : 0.0f;
 #pragma unroll
     for (int u = 0; u < kRedZ; ++u) s += v[u];
   }
