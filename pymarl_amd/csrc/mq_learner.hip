@@ -93,6 +93,8 @@ struct mq_handle {
   bool dwh_overlap = getenv("MQ_DWH_OVERLAP") && atoi(getenv("MQ_DWH_OVERLAP")) != 0;
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // A/B switch: dW_hyper launched between the mixer and the BPTT instead of after the BPTT (same stream)
+  bool dwh_first = getenv("MQ_DWH_FIRST") && atoi(getenv("MQ_DWH_FIRST")) != 0;
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
   int slots = 0;
   uint32_t mask = 0;
@@ -485,6 +487,11 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
     if (timed) MQ_HIP(hipEventRecord(h->ev1[ti], h->side));
     MQ_HIP(hipEventRecord(h->ev_join, h->side));
   }
+  const bool dwh_first = !side && c.mixer == MQ_MIXER_QMIX && !h->force_unfused_mix && h->dwh_first;
+  if (dwh_first) {
+    pt.begin(PH_DWH);
+    MQ_HIP(launch_dwh(h, d, L, w, s, false));
+  }
   pt.begin(PH_GRUB);
   if (fused_bwd) {
     // one row per workgroup: dW_hh / dW_ih / dX1 / dW1 on the chain's idle matrix cores (gru_bwd_fused.hpp)
@@ -519,7 +526,7 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
       MQ_HIP(launch_gemm(p, mq::H, d.I, ns, s));
     }
   }
-  if (c.mixer == MQ_MIXER_QMIX && !side) {
+  if (c.mixer == MQ_MIXER_QMIX && !side && !dwh_first) {
     pt.begin(PH_DWH);
     if (!h->force_unfused_mix) {
       MQ_HIP(launch_dwh(h, d, L, w, s, false));
