@@ -219,10 +219,8 @@ __global__ __launch_bounds__(HYWS_THREADS) void hyper_ws_kernel(Dims d, Rep rp, 
     uint64_t* stl = (uint64_t*)S0 + 32 * (blockIdx.y * gridDim.x + blockIdx.x) + 16;
     const bool stamp = (VAR & 1) && lw == 0 && lane == 0;
     if (stamp) stl[0] = __builtin_amdgcn_s_memtime();
-    // two register sets: chunk k is fetched into set k & 1 two chunk periods before it is staged (one period was
-    // shorter than an L2 round trip, so the MFMA waves waited on the loaders at every chunk)
-    float wr0[48], wr1[48];
-    auto fetch = [&](float (&wr)[48], int c) {
+    float wr[48];
+    auto fetch = [&](int c) {
       const int j0 = min(16 * (4 * c + lw), NH - 16);
       const HypSeg sg = hyp_seg(L, n * E, E, j0);
       const int base = (int)(sg.w + (int64_t)sg.row * S) * 4;
@@ -231,29 +229,23 @@ __global__ __launch_bounds__(HYWS_THREADS) void hyper_ws_kernel(Dims d, Rep rp, 
         wr[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(prs, voff, base + 256 * q, 0));
     };
     float* const dst0 = wst + lw * HYWS_GS + lane;
-    auto stage = [&](const float (&wr)[48], int c) {
+    auto stage = [&](int c) {
       float* dst = dst0 + (c & 1) * WB;
 #pragma unroll
       for (int q = 0; q < 48; ++q) dst[64 * q] = wr[q];
     };
-    fetch(wr0, 0);
-    if (NCH > 1) fetch(wr1, 1);
+    fetch(0);
     for (int j = lw * 64 + lane; j < NH; j += NLW * 64) {
       const HypSeg sg = hyp_seg(L, n * E, E, j);
       bias_s[j] = P[sg.b + sg.row];
     }
-    stage(wr0, 0);
-    if (NCH > 2) fetch(wr0, 2);
-    // at the barrier of chunk c: stage chunk c + 1 from set (c + 1) & 1, then refill that set with chunk c + 3
-    auto step = [&](float (&wr)[48], int c) {
+    stage(0);
+    if (NCH > 1) fetch(1);
+    for (int c = 0; c < NCH; ++c) {
       if (stamp) stl[1 + min(c, 6)] = __builtin_amdgcn_s_memtime();
       __syncthreads();   // chunk c staged; buffer (c + 1) & 1 free
-      if (c + 1 < NCH) stage(wr, c + 1);
-      if (c + 3 < NCH) fetch(wr, c + 3);
-    };
-    for (int c = 0; c < NCH; c += 2) {
-      step(wr1, c);
-      if (c + 1 < NCH) step(wr0, c + 1);
+      if (c + 1 < NCH) stage(c + 1);
+      if (c + 2 < NCH) fetch(c + 2);
     }
     if (stamp) stl[8] = __builtin_amdgcn_s_memtime();
     return;
