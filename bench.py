@@ -3,6 +3,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
 
+`--gpus N` means N ranks: launched without torch.distributed.run (WORLD_SIZE unset) and N > 1, the parent starts
+`torch.distributed.run --nproc-per-node N` as a child process before it touches the GPU and exits with its code;
+under torch.distributed.run a WORLD_SIZE different from --gpus is an error (exit 2).
+
 Metric (BASELINE.json): learner samples/s = B*T*n_agents per train() / wall seconds, whole job (all ranks).
 Default workload = BASELINE configs[1]: QMIX synthetic replay n_agents=8, T=120, obs=80, state=168, batch=32 per
 GPU (weak scaling: every rank trains its own 32-episode shard of one global sample and the ranks all-reduce the
@@ -16,6 +20,8 @@ The JSON line also carries:
   duration comes from HIP events on the learner's stream over a second timed region of the same K steps (the
   first timed region, which gives `value`, carries no events); `traffic` = PMC-measured HBM bytes per launch of
   that kernel, read from profiles/ if a pmc summary for this config is committed there (null otherwise).
+  The PMC summary is stamped with a hash of the kernel sources it measured (pymarl_amd/csrc); a summary whose hash
+  differs from the sources this bench runs is stale and is not used (traffic null, `traffic_source` says why).
 * cpu_baseline: the numpy oracle's train() (oracle/qlearner_np.py, a restatement of the reference's QLearner.train
   pinned to golden vectors of the reference itself) timed on this host, rank 0 at N=1 only, on a bounded sample.
 """
@@ -279,7 +285,35 @@ def coma_cpu_baseline(cfg_name, data, budget_s=12.0):
                       f"median {s * 1e3:.1f} ms/step, {cores} BLAS threads"}
 
 
-def init_distributed():
+def kernel_source_hash():
+    """sha256 of the kernel sources (pymarl_amd/csrc): stamps PMC summaries so a stale one is never reported."""
+    import hashlib
+    hsh = hashlib.sha256()
+    csrc = os.path.join(ROOT, "pymarl_amd", "csrc")
+    for name in sorted(os.listdir(csrc)):
+        if name.endswith((".hpp", ".hip", ".h")) or name == "Makefile":
+            hsh.update(name.encode())
+            with open(os.path.join(csrc, name), "rb") as f:
+                hsh.update(f.read())
+    for name in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        with open(os.path.join(ROOT, "include", name), "rb") as f:
+            hsh.update(f.read())
+    return hsh.hexdigest()
+
+
+def launch_ranks(a):
+    """--gpus N > 1 without torch.distributed.run: run it as a child (the parent never initialises the GPU)."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def init_distributed(expect_world=None):
     """One process per GPU (torch.distributed.run env); returns (world, rank, device)."""
     import torch as th
     import torch.distributed as dist
@@ -297,9 +331,20 @@ def init_distributed():
             dist.init_process_group("nccl", device_id=th.device("cuda", dev_index))
         else:
             dist.init_process_group(backend)
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
+    if expect_world is not None and world != expect_world:
+        raise SystemExit(f"bench.py: --gpus {expect_world} but the process group has {world} ranks")
     device = th.device("cuda", dev_index)
     th.cuda.set_device(device)
     return world, rank, device
+
+
+def dist_info(world):
+    import torch.distributed as dist
+    if world > 1 and dist.is_initialized():
+        return {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()),
+                "collective": "all_reduce(sum) of the fused [grads | sums] buffer, comm stream"}
+    return {"world_size": 1, "backend": None, "collective": None}
 
 
 def coma_bench(a):
@@ -308,7 +353,7 @@ def coma_bench(a):
     (include/mc_coma.h, mc_set_data_parallel; SURVEY.md §8e "COMA caveat")."""
     import torch as th
     import torch.distributed as dist
-    world, rank, device = init_distributed()
+    world, rank, device = init_distributed(a.gpus)
     args, buf, learner, data, mac = build_coma_workload(a.config, device, dp=world > 1)
     _, n, A, O, S, T, B, desc = CONFIGS[a.config]
     np.random.seed(2)
@@ -361,6 +406,7 @@ def coma_bench(a):
         "config": {"workload": desc, "learner": "coma_learner", "n_agents": n, "n_actions": A, "obs_dim": O,
                    "state_dim": S, "episode_limit": T, "batch_per_gpu": B, "global_batch": B * world,
                    "replay_episodes": buf.buffer_size, "parallelism": f"dp{world}"},
+        "dist": dist_info(world),
         "roofline": {"bound": "mfma", "kernel": "critic step chain (l1 + head + wgrad, x T)",
                      "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "launch_ms": chain_ms / T,
@@ -374,18 +420,27 @@ def coma_bench(a):
 
 
 def pmc_traffic(cfg_name, phase):
-    """HBM bytes per launch of `phase` from a committed PMC summary (profiles/*pmc*.json), else None."""
+    """(HBM bytes per launch of `phase`, provenance) from the newest committed PMC summary (profiles/*pmc*.json)
+    whose kernel-source hash matches the sources this run uses; (None, reason) otherwise."""
     import glob
+    want = kernel_source_hash()
+    stale = []
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
-            v = d.get(cfg_name, {}).get(phase, {}).get("hbm_bytes_per_launch")
-            if v:
-                return float(v)
         except Exception:
             continue
-    return None
+        v = d.get(cfg_name, {}).get(phase, {}).get("hbm_bytes_per_launch")
+        if not v:
+            continue
+        rel = os.path.relpath(path, ROOT)
+        if d.get("source_sha256") != want:
+            stale.append(rel)
+            continue
+        return float(v), f"{rel} (PMC FETCH_SIZE/WRITE_SIZE passes of these kernel sources, sha256 {want[:12]})"
+    return None, ("no PMC summary of these kernel sources" +
+                  (f"; stale (other sources): {', '.join(stale[:3])}" if stale else ""))
 
 
 def main():
@@ -397,13 +452,21 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--phases", action="store_true", help="print every phase's mean ms to stderr")
     a = ap.parse_args()
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        sys.exit(launch_ranks(a))
+    if int(env_world or 1) != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
+        sys.exit(2)
     if a.config == "cfg5":
         return coma_bench(a)
 
     import torch as th
     import torch.distributed as dist
 
-    world, rank, device = init_distributed()
+    world, rank, device = init_distributed(a.gpus)
     args, buf, learner, data = build_workload(a.config, device)
     mixer, n, A, O, S, T, B, desc = CONFIGS[a.config]
 
@@ -466,10 +529,10 @@ def main():
             print(json.dumps({"phase_ms": survey}), file=sys.stderr)
         fl = algorithmic_flops(dominant, n, A, O, S, T, B, mixer=mixer, fused_fwd=fused_fwd, fused_bwd=fused_bwd)
         achieved = (fl / (dom_ms * 1e-3) / 1e12) if (fl and dom_ms > 0) else None
-        traffic = pmc_traffic(a.config, dominant)
+        traffic, traffic_src = pmc_traffic(a.config, dominant)
         roof = {"bound": "mfma", "kernel": dominant, "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": (achieved / FP32_PEAK_TFLOPS) if achieved else None,
-                "traffic": traffic, "launch_ms": dom_ms, "flops_per_launch": fl,
+                "traffic": traffic, "traffic_source": traffic_src, "launch_ms": dom_ms, "flops_per_launch": fl,
                 "fused": {"fwd": fused_fwd, "bwd": fused_bwd}}
         cpu = rollout = None
         if world == 1 and not a.no_cpu_baseline:
@@ -483,6 +546,7 @@ def main():
             "config": {"workload": desc, "mixer": mixer, "n_agents": n, "n_actions": A, "obs_dim": O,
                        "state_dim": S, "episode_limit": T, "batch_per_gpu": B, "global_batch": B * world,
                        "replay_episodes": buf.buffer_size, "parallelism": f"dp{world}"},
+            "dist": dist_info(world),
             "roofline": roof,
             "hbm_roofline_whole_step": {"achieved_GBs": value * bytes_per_sample / 1e9, "peak_GBs": HBM_PEAK_GBS,
                                         "frac": value * bytes_per_sample / 1e9 / HBM_PEAK_GBS},

@@ -113,6 +113,22 @@ int mq_agent_forward(mq_handle* h, const float* inputs, int32_t rows, const floa
 int mq_greedy_actions(const float* q, const int32_t* avail, int64_t* out, int32_t rows, int32_t n_actions,
                       void* stream);
 
+/* Which kernel variants the last mq_forward_backward launched (test / profiling introspection; no device sync).
+ * rw_fwd / rw_bwd: rows per workgroup of the unfused recurrences (0 when the fused kernel ran). */
+enum { MQ_HYP_NONE = 0, MQ_HYP_WS = 1, MQ_HYP_LDS = 2, MQ_HYP_GEMM = 3 };
+enum { MQ_MIX_FAST16 = 0, MQ_MIX_FAST32 = 1, MQ_MIX_GENERIC = 2 };
+typedef struct mq_plan {
+  int32_t rows;          /* R = batch_size * n_agents */
+  int32_t fused_fwd;     /* gru_fwd_fused_kernel (1) or fc1 / gi / gru_fwd<rw_fwd> / fc2 (0) */
+  int32_t rw_fwd;
+  int32_t fused_bwd;     /* gru_bwd_fused_kernel (1) or gru_bwd<rw_bwd> / dx1 / dw1 (0) */
+  int32_t rw_bwd;
+  int32_t inline_ids;    /* episode ids in the kernel arguments (1) or read from mq_replay.ep_ids (0) */
+  int32_t hyper;         /* MQ_HYP_* */
+  int32_t mix;           /* MQ_MIX_* */
+} mq_plan;
+int mq_last_plan(const mq_handle* h, mq_plan* out);
+
 /* Optional per-kernel HIP-event timing of train steps (bench / profiling): events bracket every phase whose bit
  * is set in phase_mask (bit i = phase i of mq_phase_names), in a ring of `slots` steps; slots = 0 turns it off. */
 int mq_set_timing(mq_handle* h, int32_t slots, uint32_t phase_mask);

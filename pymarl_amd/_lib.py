@@ -26,6 +26,7 @@ EXPORTS = [
     "mq_last_error", "mq_create", "mq_destroy", "mq_param_offsets", "mq_bind", "mq_forward_backward", "mq_apply",
     "mq_train_step", "mq_update_targets", "mq_copy_intermediate", "mq_mac_forward", "mq_agent_forward",
     "mq_greedy_actions", "mq_set_timing", "mq_phase_times", "mq_phase_names", "mq_set_data_parallel",
+    "mq_last_plan",
     # include/mc_coma.h
     "mc_create", "mc_destroy", "mc_param_offsets", "mc_bind", "mc_train_step", "mc_update_targets", "mc_policy",
     "mc_copy_intermediate", "mc_set_timing", "mc_phase_times", "mc_set_data_parallel",
@@ -73,6 +74,17 @@ class MCConfig(ctypes.Structure):
     ]
 
 
+class MQPlan(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int32) for k in ("rows", "fused_fwd", "rw_fwd", "fused_bwd", "rw_bwd", "inline_ids",
+                                               "hyper", "mix")]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+HYP_NAMES = {0: "none", 1: "ws", 2: "lds", 3: "gemm"}
+MIX_NAMES = {0: "fast16", 1: "fast32", 2: "generic"}
+
 INLINE_IDS = 256   # MQ_INLINE_IDS: batches up to this size pass their episode ids in the kernel arguments
 
 
@@ -112,6 +124,7 @@ def load(required=True):
         "mq_greedy_actions": ([vp, vp, vp, i32, i32, vp], ctypes.c_int),
         "mq_set_timing": ([vp, i32, ctypes.c_uint32], ctypes.c_int),
         "mq_set_data_parallel": ([vp, i32], ctypes.c_int),
+        "mq_last_plan": ([vp, ctypes.POINTER(MQPlan)], ctypes.c_int),
         "mq_phase_times": ([vp, ctypes.POINTER(ctypes.c_float), i32, ctypes.POINTER(i32)], ctypes.c_int),
         "mc_create": ([ctypes.POINTER(MCConfig), ctypes.POINTER(vp)], ctypes.c_int),
         "mc_destroy": ([vp], ctypes.c_int),

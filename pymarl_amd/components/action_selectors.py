@@ -58,8 +58,8 @@ class EpsilonGreedyActionSelector:
         if test_mode:
             self.epsilon = 0.0
         greedy = greedy_actions(agent_inputs, avail_actions)
-        if self.epsilon <= 0.0:
-            return greedy
+        # both draws happen in test mode too (epsilon 0), as in the reference (:57-59): the torch RNG stream then
+        # stays the reference's across interleaved test episodes
         random_numbers = th.rand_like(agent_inputs[:, :, 0])
         pick_random = (random_numbers < self.epsilon).long()
         random_actions = Categorical(avail_actions.float()).sample().long()

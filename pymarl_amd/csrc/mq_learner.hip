@@ -81,6 +81,7 @@ struct mq_handle {
   // last step bookkeeping
   bool have_fb = false;
   Dims last;
+  mq_plan plan{};
   int nsplit_fc1 = 1, nsplit_mix = 1, nblk_bwd = 1, nblk_mix = 1, n_norm_part = 0;
   bool force_unfused = getenv("MQ_UNFUSED_FWD") != nullptr;       // A/B switch for the fused agent forward
   bool force_unfused_bwd = getenv("MQ_UNFUSED_BWD") != nullptr;   // A/B switch for the fused BPTT
@@ -404,13 +405,18 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   PhaseTimer pt{h, s};
   const mq_config& c = h->cfg;
 
+  mq_plan plan{};
+  plan.rows = d.R;
+  plan.inline_ids = rp.nids > 0 ? 1 : 0;
   const int rw_fwd = pick_rw(d.R, 512);
   if (rw_fwd == 1 && fused_fwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused) {
+    plan.fused_fwd = 1;
     // one row per workgroup: fc1 / W_ih / fc2 ride on the recurrence's idle matrix cores (gru_fwd_fused.hpp)
     pt.begin(PH_GRUF);
     launch_fwd_fused(dim3(d.R, 2), s, d, rp, (const float*)h->on, (const float*)h->tg, L, w);
     MQ_HIP(hipGetLastError());
   } else {
+    plan.rw_fwd = rw_fwd;
     pt.begin(PH_FC1);
     {
       Fc1Prob p{d, rp, h->on, h->tg, h->off[MQ_P_FC1_W], h->off[MQ_P_FC1_B], w.X1, w.XIN, RT};
@@ -438,17 +444,20 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   if (c.mixer == MQ_MIXER_QMIX) {
     pt.begin(PH_HYP);
     if (hyper_ws_ok(d.S, d.E, d.NH, d.M) && !h->force_unfused_mix) {
+      plan.hyper = MQ_HYP_WS;
       // wave-specialised weight streaming (hyper_kernel.hpp)
       hipLaunchKernelGGL(hyper_ws_kernel<0>, dim3((d.M + HYR - 1) / HYR, 2), dim3(HYWS_THREADS),
                          hyper_ws_lds_bytes(d.S), s, d, rp, (const float*)h->on, (const float*)h->tg, L, w.HYP,
                          w.S0);
       MQ_HIP(hipGetLastError());
     } else if (hyper_ok(d.S, d.NH) && !h->force_unfused_mix) {
+      plan.hyper = MQ_HYP_LDS;
       const size_t dyn = HyperGeom(d.S, d.NH).lds_bytes();
       hipLaunchKernelGGL(hyper_kernel<0>, dim3((d.M + HYR - 1) / HYR, 2), dim3(256), dyn, s, d, rp,
                          (const float*)h->on, (const float*)h->tg, L, w.HYP, w.S0);
       MQ_HIP(hipGetLastError());
     } else {
+      plan.hyper = MQ_HYP_GEMM;
       HypProb p{d, rp, L, h->on, h->tg, w.HYP, w.S0};
       MQ_HIP(launch_gemm(p, d.M, d.NH, 2, s));
     }
@@ -457,6 +466,7 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   h->nblk_mix = (d.M + 3) / 4;
   {
     const bool fast = d.n <= 16 && d.E <= 64 && !h->generic_mix;
+    plan.mix = fast && d.A <= 16 ? MQ_MIX_FAST16 : fast && d.A <= 32 ? MQ_MIX_FAST32 : MQ_MIX_GENERIC;
     if (fast && d.A <= 16)
       hipLaunchKernelGGL((mix_fast_kernel<16, 16>), dim3(h->nblk_mix), dim3(256), 0, s, d, rp, (const float*)h->on,
                          (const float*)h->tg, L, w, curmax);
@@ -493,6 +503,8 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
     MQ_HIP(launch_dwh(h, d, L, w, s, false));
   }
   pt.begin(PH_GRUB);
+  plan.fused_bwd = fused_bwd ? 1 : 0;
+  plan.rw_bwd = fused_bwd ? 0 : rw_bwd;
   if (fused_bwd) {
     // one row per workgroup: dW_hh / dW_ih / dX1 / dW1 on the chain's idle matrix cores (gru_bwd_fused.hpp)
     h->nblk_bwd = d.R;
@@ -562,6 +574,7 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   }
   pt.end();
   h->last = d;
+  h->plan = plan;
   h->have_fb = true;
   return MQ_OK;
 }
@@ -585,6 +598,13 @@ int mq_apply(mq_handle* h, void* stream) {
   MQ_HIP(hipGetLastError());
   pt.end();
   ++h->tstep;
+  return MQ_OK;
+}
+
+int mq_last_plan(const mq_handle* h, mq_plan* out) {
+  if (!h || !out) return set_err(MQ_ERR_ARG, "NULL argument");
+  if (!h->have_fb) return set_err(MQ_ERR_STATE, "no forward/backward has run");
+  *out = h->plan;
   return MQ_OK;
 }
 

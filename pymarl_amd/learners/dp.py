@@ -4,8 +4,16 @@ Every rank backpropagates the UNNORMALISED loss sum (td*m)^2 of its shard; the g
 mask / stats sums in its tail (include/mq_learner.h, MQ_NSUMS). Summing that single buffer across ranks and
 dividing by the global sum(mask) afterwards reproduces the reference's global normalisation
 loss = sum (td*m)^2 / sum(m) (q_learner.py:97) exactly — averaging per-rank losses would not.
+
+On a GPU the collective is issued on a dedicated communication stream: it waits on an event recorded after the
+reduction kernels on the compute stream, and the compute stream waits on an event recorded after it, before
+mq_apply. Nothing on the compute stream is serialised behind RCCL's own stream beyond that one dependency, and the
+host never blocks.
 """
+import torch
 import torch.distributed as dist
+
+_COMM = {}
 
 
 def shard_bounds(batch_size, rank, world):
@@ -13,8 +21,32 @@ def shard_bounds(batch_size, rank, world):
     return rank * batch_size // world, (rank + 1) * batch_size // world
 
 
+def comm_stream(device):
+    """The per-device communication stream (created once, highest priority: it gates mq_apply)."""
+    key = torch.device(device).index
+    if key not in _COMM:
+        lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
+        _COMM[key] = torch.cuda.Stream(device=device, priority=min(lo, hi))
+    return _COMM[key]
+
+
 def allreduce_grad_buffer(buf, group=None):
-    """Sum the fused [grads | sums] buffer over the process group (RCCL over xGMI on MI355X; gloo on CPU)."""
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    """Sum the fused [grads | sums] buffer over the process group (RCCL over xGMI on MI355X; gloo on CPU).
+    GPU buffers: on the communication stream, event-joined both ways with the current (compute) stream."""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1):
+        return buf
+    if buf.is_cuda and dist.get_backend(group) == "nccl":
+        compute = torch.cuda.current_stream(buf.device)
+        comm = comm_stream(buf.device)
+        ready = torch.cuda.Event()
+        ready.record(compute)
+        comm.wait_event(ready)
+        with torch.cuda.stream(comm):
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+            done = torch.cuda.Event()
+            done.record(comm)
+        buf.record_stream(comm)
+        compute.wait_event(done)
+    else:
         dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
     return buf

@@ -206,8 +206,7 @@ class QLearner:
             self._curmax = th.zeros(Tmax * need_b * self.args.n_agents, dtype=th.int32, device=self._online.device)
             _lib.check(h.lib.mq_bind(h.h, _lib.ptr(self._online), _lib.ptr(self._target), _lib.ptr(self._grad),
                                      _lib.ptr(self._sq), _lib.ptr(self._stats), _lib.ptr(self._curmax)))
-            if self._dp_active() or getattr(self, "force_dp_norm", False):
-                _lib.check(h.lib.mq_set_data_parallel(h.h, 1))
+            h.dp_on = False
             if h.n_params != self.n_params:
                 raise _lib.MQError("parameter layout mismatch: library {} vs modules {}".format(h.n_params,
                                                                                               self.n_params))
@@ -218,10 +217,17 @@ class QLearner:
     def train(self, batch, t_env: int, episode_num: int):
         _lib.require_gpu(self._online)
         h = self._get_handle(batch)
+        # decided per call: torch.distributed may be initialised after the handle was created; mq_apply must then
+        # recompute the gradient norm from the all-reduced buffer
+        dp = self._dp_active()
+        want = dp or getattr(self, "force_dp_norm", False)
+        if want != h.dp_on:
+            _lib.check(h.lib.mq_set_data_parallel(h.h, int(want)))
+            h.dp_on = want
         rep, keep = replay_view(batch)
         lib, s = h.lib, _lib.stream_ptr()
         _lib.check(lib.mq_forward_backward(h.h, ctypes.byref(rep), s))
-        if self.dp:
+        if dp:
             allreduce_grad_buffer(self._grad)
         _lib.check(lib.mq_apply(h.h, s))
         self._opt_steps += 1
@@ -292,6 +298,16 @@ class QLearner:
         st = self._stats.tolist()
         return dict(loss=st[0], grad_norm=st[1], td_error_abs=st[2], q_taken_mean=st[3], target_mean=st[4],
                     mask_sum=st[5])
+
+    def last_plan(self):
+        """Kernel variants the last train() launched (mq_last_plan): rows, fused_fwd, rw_fwd, fused_bwd, rw_bwd,
+        inline_ids, hyper, mix."""
+        pl = _lib.MQPlan()
+        _lib.check(self._handle.lib.mq_last_plan(self._handle.h, ctypes.byref(pl)))
+        d = pl.as_dict()
+        d["hyper"] = _lib.HYP_NAMES[d["hyper"]]
+        d["mix"] = _lib.MIX_NAMES[d["mix"]]
+        return d
 
     def last_cur_max_actions(self):
         """Double-Q greedy actions of the last step as (B, T, n) int64 (q_learner.py:75)."""

@@ -180,7 +180,7 @@ def run_case(name, case):
     args, buf, mac, learner, logger = build(case)
     np.random.seed(case["sampler_seed"])
     out = {k: np.array(v) for k, v in case.items() if not isinstance(v, str)}
-    out["mixer"] = np.array(case["mixer"])
+    out["mixer"] = np.array(case["mixer"] or "none")   # IQL (mixer: None, iql_smac.yaml:21) is stored as "none"
     if case.get("store_params", True):
         out["params_init"] = flat_params(learner)
     ids_all, losses, full = [], [], case["full"]
@@ -217,6 +217,11 @@ def run_case(name, case):
             acts = [mac.select_actions(batch, t_ep=t, t_env=0, test_mode=True).numpy() for t in range(t_all)]
             out["greedy_actions"] = np.stack(acts, 1).astype(np.int64)
         learner.train(batch, t_env=1000 * k, episode_num=episodes[k])
+        if k == case.get("ckpt_step", -1):
+            # the reference's own checkpoint files (q_learner.py:131-135, basic_controller.py:91-92)
+            ck = os.path.join(HERE, "ckpt_{}_step{}".format(name, k))
+            os.makedirs(ck, exist_ok=True)
+            learner.save_models(ck)
         losses.append(logger.stats["loss"][-1])
         assert abs(losses[-1] - inter["loss"]) <= 1e-6 * max(1.0, abs(losses[-1])), (losses[-1], inter["loss"])
         if full and k == 0:
@@ -255,9 +260,25 @@ CFG3 = dict(n=27, A=36, O=285, S=1170, T=180, B=4, n_episodes=8, data_seed=0, we
 CFG4 = dict(n=5, A=11, O=80, S=120, T=120, B=64, n_episodes=96, data_seed=0, weight_seed=1, sampler_seed=2,
             ragged=False, steps=4, episodes=[0, 8, 200, 208], full=False, record_actions_steps=2)
 
+# Batches past the fused kernels' row limits (R = B * n rows): R in (512, 1024] runs gru_fwd_kernel<2>, (1024, 2048]
+# gru_fwd_kernel<4>, > 2048 gru_fwd_kernel<8>; B > 256 (MQ_INLINE_IDS) passes the episode ids as a device vector.
+# Small O / S / T keep the reference's CPU run short.
+WIDE = dict(data_seed=3, weight_seed=4, sampler_seed=5, ragged=True, steps=3, episodes=[0, 8, 200], full=False,
+            record_actions_steps=3)
+
 CASES = {
-    "tiny_qmix": dict(TINY, mixer="qmix"),
-    "tiny_vdn": dict(TINY, mixer="vdn"),
+    "tiny_qmix": dict(TINY, mixer="qmix", ckpt_step=2),
+    "tiny_vdn": dict(TINY, mixer="vdn", ckpt_step=2),
+    # IQL (src/config/algs/iql_smac.yaml:21, mixer: None): the loss normaliser is n_agents * sum(mask)
+    # (q_learner.py:89-97, mask.expand_as(td_error))
+    "tiny_iql": dict(TINY, mixer=None),
+    "cfg2_iql": dict(CFG2, mixer=None, steps=10, episodes=[8 * k for k in range(5)] + [200 + k for k in range(5)]),
+    "rw2_qmix": dict(WIDE, n=8, A=6, O=12, S=20, T=12, B=72, n_episodes=96, mixer="qmix"),
+    "rw4_vdn": dict(WIDE, n=16, A=7, O=10, S=16, T=10, B=80, n_episodes=100, mixer="vdn"),
+    "wide_qmix": dict(WIDE, n=8, A=5, O=8, S=12, T=8, B=300, n_episodes=320, mixer="qmix"),
+    # BASELINE configs[2] exactly (27m_vs_30m shape, VDN, B = 128): R = 3456 rows, the bench's kernel path
+    "cfg3_vdn_b128": dict(CFG3, mixer="vdn", B=128, n_episodes=136, steps=2, episodes=[0, 8], ragged=True,
+                          record_actions_steps=1),
     "tiny_qmix_full": dict(TINY, mixer="qmix", ragged=False, n_episodes=4, steps=3, episodes=[0, 200, 201]),
     "cfg2_qmix": dict(CFG2, mixer="qmix"),
     "cfg2_vdn": dict(CFG2, mixer="vdn", steps=10, episodes=[8 * k for k in range(5)] + [200 + k for k in range(5)]),

@@ -10,7 +10,8 @@ from pymarl_amd.utils.synthetic import agent_param_shapes, init_params, make_rep
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASE_NAMES = ["tiny_qmix", "tiny_vdn", "tiny_qmix_full", "cfg2_qmix", "cfg2_vdn", "cfg2_qmix_ragged",
-              "cfg3_vdn", "cfg3_qmix", "cfg4_qmix"]
+              "cfg3_vdn", "cfg3_qmix", "cfg4_qmix", "tiny_iql", "cfg2_iql", "rw2_qmix", "rw4_vdn", "wide_qmix",
+              "cfg3_vdn_b128"]
 
 
 class Case:

@@ -14,6 +14,9 @@ from pymarl_amd.learners import REGISTRY as le_REGISTRY
 from pymarl_amd.utils.logging import Logger
 
 
+CKPT = {name: "ckpt_{}_step2".format(name) for name in ("tiny_qmix", "tiny_vdn")}
+
+
 def make_args(case, **over):
     a = SN(n_agents=case.n, n_actions=case.A, state_shape=case.S, obs_shape=case.O, rnn_hidden_dim=64,
            mixing_embed_dim=32, mixer=None if case.mixer == "none" else case.mixer, lr=5e-4, optim_alpha=0.99,
@@ -46,7 +49,8 @@ def build(case, device="cuda", **over):
     mac = mac_REGISTRY["basic_mac"](buf.scheme, groups, args)
     logger = Logger(logging.getLogger("mq-test"))
     learner = le_REGISTRY["q_learner"](mac, buf.scheme, logger, args)
-    learner.cuda()
+    if device != "cpu":
+        learner.cuda()
     sd = {k: th.from_numpy(v) for k, v in case.agent_params.items()}
     mac.agent.load_state_dict(sd)
     learner.target_mac.agent.load_state_dict(sd)

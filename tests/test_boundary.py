@@ -40,6 +40,7 @@ int main(void) {
   printf("%d %d\\n", MQ_P_COUNT, MQ_NSUMS);
   printf("%zu %zu %zu %d %d %d\\n", sizeof(mc_config), offsetof(mc_config, gamma), offsetof(mc_config, max_seq),
          MC_P_COUNT, MC_NTAIL, MC_NSTATS);
+  printf("%zu %zu %zu\\n", sizeof(mq_plan), offsetof(mq_plan, inline_ids), offsetof(mq_plan, mix));
   return 0;
 }
 """)
@@ -50,7 +51,8 @@ int main(void) {
     py = [ctypes.sizeof(_lib.MQConfig), _lib.MQConfig.gamma.offset, _lib.MQConfig.max_seq.offset,
           ctypes.sizeof(_lib.MQReplay), _lib.MQReplay.batch_size.offset, _lib.P_COUNT, _lib.NSUMS,
           ctypes.sizeof(_lib.MCConfig), _lib.MCConfig.gamma.offset, _lib.MCConfig.max_seq.offset, _lib.MC_P_COUNT,
-          _lib.MC_NTAIL, _lib.MC_NSTATS]
+          _lib.MC_NTAIL, _lib.MC_NSTATS, ctypes.sizeof(_lib.MQPlan), _lib.MQPlan.inline_ids.offset,
+          _lib.MQPlan.mix.offset]
     assert c == py
 
 
@@ -78,3 +80,4 @@ def test_train_without_handle_bound_reports_state_error():
     lib = _lib.load()
     assert lib.mq_apply(None, None) != 0
     assert lib.mq_forward_backward(None, None, None) != 0
+    assert lib.mq_last_plan(None, ctypes.byref(_lib.MQPlan())) != 0

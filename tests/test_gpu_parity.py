@@ -3,20 +3,26 @@
 Runs through the product path: QLearner.train -> libmq_learner.so (C ABI) on an MI355X.
 
 Two kinds of check (DESIGN.md "Parity"):
-* free-running trajectory vs the reference's golden run: loss / stats 1e-4 relative for the first TIGHT_STEPS
-  steps, a 2x loss band after. Two discrete decisions sit on fp32 rounding: the double-Q target gathers the
-  TARGET net's Q at the ONLINE net's argmax (q_learner.py:75-76), and the fc1 relu (rnn_agent.py:28) switches at
-  0. A near-tie that rounds the other way (1 in ~10^6 decisions; which one depends on the summation order of the
-  fc1 / mixer contractions) changes a target by O(1) or a gradient row, and RMSprop's per-parameter
-  normalisation carries it into the next step's parameters at O(lr): from the first such event on, the GPU and
-  the reference follow different, equally valid trajectories. The free run therefore pins step 0 (identical
-  starting state) tightly and the rest loosely.
+* free-running trajectory vs the reference's golden run. north_star asks for the loss trajectory to 1e-4 relative.
+  Two discrete decisions sit on fp32 rounding: the double-Q target gathers the TARGET net's Q at the ONLINE net's
+  argmax (q_learner.py:75-76), and the fc1 relu (rnn_agent.py:28) switches at 0. A near-tie that rounds the other
+  way changes a target by O(1) or a gradient row, and RMSprop's per-parameter normalisation carries it into the
+  next step's parameters at O(lr): from the first such event on, the GPU and the reference follow different,
+  equally valid trajectories (the oracle and the reference themselves part after 12 cfg2 steps). So at every step
+  the oracle is run from the GPU's own state and every decision is classified: a near-tie (top-2 margin
+  <= MARGIN_EPS * max(1, |Q|), or |fc1 pre-activation| <= RELU_EPS) is exempt, and a flip (the GPU deciding a
+  near-tie the other way) is counted. The loss must hold 1e-4 against the reference for HOLD_STEPS steps, or up to
+  a step at or after the first counted flip. The per-step errors and counts are written to $MQ_PARITY_DIR.
 * teacher-forced steps (the per-step parity proper): the GPU learner and the numpy oracle (itself pinned to the
   reference at ~1e-7) start every step from the SAME parameters / optimiser state; the GPU's double-Q argmax
   must equal the oracle's wherever the top-2 margin exceeds MARGIN_EPS and its fc1 relu decisions wherever
   |pre-activation| > RELU_EPS; the oracle then follows the GPU's decisions on the near-ties, and loss / stats
-  must agree to 1e-5 relative, gradients and updated parameters to 1e-4 / 1e-5 of the tensor max.
+  must agree to 1e-5 relative, gradients and updated parameters to 1e-4 / 1e-5 of the tensor max. The exempted
+  near-ties and the flips among them are counted per step and written out.
 """
+import json
+import os
+
 import numpy as np
 import pytest
 import torch as th
@@ -26,9 +32,57 @@ from tests.golden_utils import Case
 pytestmark = pytest.mark.gpu
 
 STATS = ["loss", "grad_norm", "td_error_abs", "q_taken_mean", "target_mean"]
-MARGIN_EPS = 1e-4
+MARGIN_EPS = 1e-5   # argmax-equal wherever the top-2 gap exceeds 1e-5 * max(1, |Q|)
 RELU_EPS = 1e-5
-TIGHT_STEPS = 1
+HOLD_STEPS = 12     # the oracle itself holds the reference's cfg2 loss trajectory to 1e-4 for 12 steps
+LOSS_RTOL = 1e-4    # north_star: "loss trajectory to 1e-4 rel on a fixed seed"
+
+
+def write_record(kind, name, rec):
+    out = os.environ.get("MQ_PARITY_DIR")
+    if not out:
+        return
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "parity_{}_{}.json".format(kind, name)), "w") as f:
+        json.dump(rec, f, indent=1)
+
+
+def classify_decisions(learner, o, nb, fw):
+    """Compare the GPU's double-Q argmax and fc1 relu decisions with the oracle's at the same state.
+    Returns (record, dq_flip_mask_ok, relu_flip_ok): the counts of decisions, near-ties and flips."""
+    from oracle.qlearner_np import fc1_preacts
+    q = fw["mac_out"].copy()
+    q[nb["avail_actions"] == 0] = -9999999.0
+    top2 = -np.sort(-q[:, 1:], axis=3)[..., :2]
+    margin = top2[..., 0] - top2[..., 1]
+    tie = margin <= MARGIN_EPS * np.maximum(1.0, np.abs(top2[..., 0]))
+    got = learner.last_cur_max_actions().cpu().numpy()
+    dq_flip = got != fw["cur_max_actions"]
+    on_gpu = learner.last_intermediate(3).cpu().numpy() > 0
+    pre = fc1_preacts(o.p, nb["obs"], nb["actions_onehot"])
+    relu_tie = np.abs(pre) <= RELU_EPS
+    relu_flip = on_gpu != (pre > 0)
+    rec = dict(dq_decisions=int(tie.size), dq_ties=int(tie.sum()), dq_flips=int(dq_flip.sum()),
+               dq_flips_outside_ties=int((dq_flip & ~tie).sum()), relu_decisions=int(relu_tie.size),
+               relu_ties=int(relu_tie.sum()), relu_flips=int(relu_flip.sum()),
+               relu_flips_outside_ties=int((relu_flip & ~relu_tie).sum()),
+               max_flip_pre=float(np.abs(pre[relu_flip]).max()) if relu_flip.any() else 0.0)
+    return rec, got, on_gpu
+
+
+def oracle_from_learner(o, case, learner):
+    """Put the GPU learner's params / targets / RMSprop state into the oracle (for decisions at the GPU's state)."""
+    from tests.gpu_helpers import flat_params, flat_targets
+    for which, flat in (("p", flat_params(learner)), ("t", flat_targets(learner)),
+                        ("sq", learner._sq.detach().cpu().numpy().copy())):
+        d = case.unflatten(flat)
+        for k, v in d.items():
+            if which == "sq":
+                o.sq[k] = v.astype(np.float32).copy()
+            elif k in o.p or k in o.tp:
+                (o.p if which == "p" else o.tp)[k] = v.astype(np.float32).copy()
+            else:
+                (o.mp if which == "p" else o.tmp)[k] = v.astype(np.float32).copy()
 
 
 @pytest.fixture(scope="module")
@@ -42,30 +96,44 @@ def get_case(cases, name):
     return cases[name]
 
 
-def run_case(case, check_full):
+def run_case(case, check_full, plan=None):
+    from oracle.qlearner_np import OracleQLearner
     from tests.gpu_helpers import build, flat_grads, flat_params, flat_targets, rel
     args, buf, mac, learner, logger = build(case)
+    o = OracleQLearner(case.agent_params, case.mixer_params, case.cfg())
     np.random.seed(case.sampler_seed)
+    rec = []
     for k in range(case.steps):
         batch = buf.sample(case.B)
         assert np.array_equal(batch.ep_ids_np, case.z["ids"][k]), "sampler ids diverged from the reference"
         max_t = batch.max_t_filled()
         batch = batch[:, :max_t]
+        nb, _ = case.batch(k)
+        oracle_from_learner(o, case, learner)   # the oracle's decisions at the GPU's own state
+        fw = o.forward(nb)
         learner.train(batch, 1000 * k, case.episodes[k])
+        if plan is not None and k == 0:
+            got_plan = learner.last_plan()
+            for key, v in plan.items():
+                assert got_plan[key] == v, (case.name, key, got_plan)
         st = learner.last_stats()
-        for s in STATS:
-            ref = case.z["stat_" + s][k]
-            assert np.isfinite(st[s]), (case.name, k, s)
-            if k < TIGHT_STEPS:
-                assert abs(st[s] - ref) <= 1e-4 * abs(ref) + 1e-6, (case.name, k, s, st[s], ref)
-        if k >= TIGHT_STEPS:   # a different valid trajectory after the first near-tie flip: sanity bound only
-            ref = case.z["stat_loss"][k]
-            assert 0.5 * ref <= st["loss"] <= 2.0 * ref, (case.name, k, st["loss"], ref)
-        if "cur_max_actions" in case.z and k < min(TIGHT_STEPS, case.z["cur_max_actions"].shape[0]):
+        r, _, _ = classify_decisions(learner, o, nb, fw)
+        r["step"] = k
+        r["loss"] = st["loss"]
+        r["ref_loss"] = float(case.z["stat_loss"][k])
+        for s_ in STATS:
+            ref = float(case.z["stat_" + s_][k])
+            assert np.isfinite(st[s_]), (case.name, k, s_)
+            r["rel_err_" + s_] = abs(st[s_] - ref) / max(abs(ref), 1e-12)
+        if "cur_max_actions" in case.z and k < case.z["cur_max_actions"].shape[0]:
             got = learner.last_cur_max_actions().cpu().numpy()
             ref = case.z["cur_max_actions"][k].astype(np.int64)
-            clear = case.z["margin"][k] > 1e-5 * np.maximum(1.0, np.abs(case.z["margin"][k]))
-            assert np.array_equal(got[clear], ref[clear]), (case.name, k, int((got != ref)[clear].sum()))
+            mo = learner.last_intermediate(0).cpu().numpy()[:, 1:max_t]
+            mo = np.where(nb["avail_actions"][:, 1:] == 0, np.float32(-9999999.0), mo)
+            clear = case.z["margin"][k] > MARGIN_EPS * np.maximum(1.0, np.abs(mo.max(axis=3)))
+            r["ref_dq_mismatch_clear"] = int((got != ref)[clear].sum())
+            r["ref_dq_mismatch_ties"] = int((got != ref)[~clear].sum())
+        rec.append(r)
         if check_full and k == 0:
             mo = learner.last_intermediate(0).cpu().numpy()
             assert rel(mo, case.z["step0_mac_out"]) < 2e-5
@@ -76,22 +144,86 @@ def run_case(case, check_full):
             assert rel(flat_grads(learner), case.z["step0_grads_clipped"]) < 1e-4
         if "step_params" in case.z:
             assert rel(flat_params(learner), case.z["step_params"][k]) < 1e-4, (case.name, k)
+    write_record("freerun", case.name, rec)
+    # every decision the GPU takes differently from the oracle at its own state is a near-tie
+    for r in rec:
+        assert r["dq_flips_outside_ties"] == 0 and r["relu_flips_outside_ties"] == 0, (case.name, r)
+        assert r.get("ref_dq_mismatch_clear", 0) == 0, (case.name, r)
+    # the loss trajectory holds LOSS_RTOL for HOLD_STEPS steps, or up to a counted flip
+    errs = [r["rel_err_loss"] for r in rec]
+    hold = next((k for k, e in enumerate(errs) if e > LOSS_RTOL), len(errs))
+    assert hold >= 1, (case.name, "step 0 loss", errs[0])
+    for s_ in STATS:
+        assert rec[0]["rel_err_" + s_] <= LOSS_RTOL + 1e-6 / max(abs(float(case.z["stat_" + s_][0])), 1e-6), \
+            (case.name, s_, rec[0])
+    if hold < min(HOLD_STEPS, case.steps):
+        flips = [r["dq_flips"] + r["relu_flips"] + r.get("ref_dq_mismatch_ties", 0) for r in rec[:hold + 1]]
+        assert any(flips), (case.name, "loss left 1e-4 at step {} with no counted flip before it".format(hold), errs)
+    for k in range(hold, case.steps):   # a different valid trajectory after a near-tie flip: sanity bound only
+        ref = case.z["stat_loss"][k]
+        assert 0.5 * ref <= rec[k]["loss"] <= 2.0 * ref, (case.name, k, errs)
     if "targets_final" in case.z:
-        tol = 1e-4 if case.steps <= TIGHT_STEPS else 2e-1
+        tol = 1e-4 if hold >= case.steps else 2e-1
         assert rel(flat_targets(learner), case.z["targets_final"]) < tol
     if "sqavg_final" in case.z:
         assert rel(learner._sq.cpu().numpy(), case.z["sqavg_final"]) < 1e-4
     return learner
 
 
-@pytest.mark.parametrize("name", ["tiny_qmix_full", "tiny_qmix", "tiny_vdn"])
+@pytest.mark.parametrize("name", ["tiny_qmix_full", "tiny_qmix", "tiny_vdn", "tiny_iql"])
 def test_tiny_full(cases, name):
     run_case(get_case(cases, name), check_full=True)
 
 
-@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_vdn", "cfg2_qmix_ragged", "cfg3_vdn", "cfg3_qmix", "cfg4_qmix"])
+@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_vdn", "cfg2_qmix_ragged", "cfg2_iql", "cfg3_vdn", "cfg3_qmix",
+                                  "cfg4_qmix"])
 def test_cfg2_trajectory(cases, name):
     run_case(get_case(cases, name), check_full=False)
+
+
+# Kernel variants past the fused kernels' limits, each pinned to a reference golden run (tests/golden/make_golden.py)
+# and to the oracle teacher-forced: R = B * n rows selects gru_fwd_kernel<RW> (RW = 2 / 4 / 8 rows per workgroup)
+# and gru_bwd_kernel<2>; B > 256 sends the episode ids through the device vector; cfg3_vdn_b128 is BASELINE
+# configs[2] itself (the bench's cfg3 path).
+WIDE_PLANS = {
+    "rw2_qmix": dict(rows=576, fused_fwd=0, rw_fwd=2, fused_bwd=0, rw_bwd=2, inline_ids=1, hyper="ws"),
+    "rw4_vdn": dict(rows=1280, fused_fwd=0, rw_fwd=4, fused_bwd=0, rw_bwd=2, inline_ids=1, mix="fast16"),
+    "wide_qmix": dict(rows=2400, fused_fwd=0, rw_fwd=8, fused_bwd=0, rw_bwd=2, inline_ids=0),
+    "cfg3_vdn_b128": dict(rows=3456, fused_fwd=0, rw_fwd=8, fused_bwd=0, rw_bwd=2, inline_ids=1, mix="generic"),
+    "cfg2_iql": dict(rows=256, fused_fwd=1, fused_bwd=1, hyper="none"),
+}
+
+
+@pytest.mark.parametrize("name", sorted(WIDE_PLANS))
+def test_wide_batch_paths_vs_reference(cases, name):
+    run_case(get_case(cases, name), check_full=False, plan=WIDE_PLANS[name])
+
+
+@pytest.mark.parametrize("name", ["tiny_qmix", "tiny_vdn"])
+def test_train_from_reference_checkpoint(cases, name):
+    """Load the checkpoint the REFERENCE wrote after golden step 2 (weights_only), train golden step 3 on the GPU
+    and match the reference's step-3 stats, parameters and RMSprop state (row f4, q_learner.py:131-143)."""
+    import os
+    from pymarl_amd.components.episode_buffer import SampledBatch
+    from tests.golden_utils import GOLDEN
+    from tests.gpu_helpers import CKPT, build, flat_params, rel
+    case = get_case(cases, name)
+    args, buf, mac, learner, logger = build(case)
+    learner.load_models(os.path.join(GOLDEN, CKPT[name]))
+    if learner.mixer is not None:
+        # load_models restores the target agent only (q_learner.py:137-142); in the reference's run the target
+        # mixer equals the online one after the step-2 target update (episode 200), so the test sets it so
+        learner.target_mixer.load_state_dict(learner.mixer.state_dict())
+    learner.last_target_update_episode = case.episodes[2]
+    batch = SampledBatch(buf, case.z["ids"][3])
+    batch = batch[:, :batch.max_t_filled()]
+    learner.train(batch, 3000, case.episodes[3])
+    st = learner.last_stats()
+    for s_ in STATS:
+        ref = float(case.z["stat_" + s_][3])
+        assert abs(st[s_] - ref) <= 1e-4 * abs(ref) + 1e-6, (name, s_, st[s_], ref)
+    assert rel(flat_params(learner), case.z["step_params"][3]) < 1e-4
+    assert rel(learner._sq.cpu().numpy(), case.z["sqavg_final"]) < 1e-4
 
 
 def test_greedy_select_actions(cases):
@@ -138,6 +270,9 @@ UNFUSED_ENV = ("MQ_UNFUSED_FWD", "MQ_UNFUSED_BWD", "MQ_GEMM_HYPER")
     ("tiny_vdn", 4, False),
     # BASELINE configs[2] / configs[3] shapes: the row-batched (unfused) recurrences and the GEMM path run here
     ("cfg3_vdn", 4, False), ("cfg3_qmix", 3, False), ("cfg4_qmix", 4, False),
+    # IQL (mixer None) and the kernel variants past the fused limits (WIDE_PLANS), reference-pinned cases
+    ("tiny_iql", 4, False), ("cfg2_iql", 4, False), ("rw2_qmix", 3, False), ("rw4_vdn", 3, False),
+    ("wide_qmix", 3, False), ("cfg3_vdn_b128", 2, False),
     # the A/B switches: the unfused kernel sequence on the shapes the fused kernels normally take
     ("cfg2_qmix", 4, True), ("cfg2_qmix_ragged", 3, True), ("tiny_vdn", 2, True)])
 def test_teacher_forced_steps(cases, name, steps, unfused, monkeypatch):
@@ -146,7 +281,7 @@ def test_teacher_forced_steps(cases, name, steps, unfused, monkeypatch):
 
 def run_teacher_forced(case, steps, unfused, monkeypatch):
     """Every step from the oracle's state; decisions, stats, gradients and the RMSprop step checked (see module doc)."""
-    from oracle.qlearner_np import OracleQLearner, fc1_preacts
+    from oracle.qlearner_np import OracleQLearner
     from tests.gpu_helpers import build, flat_grads, flat_params, rel
     name = case.name
     for k in UNFUSED_ENV:   # read once, at handle creation (mq_create)
@@ -157,6 +292,7 @@ def run_teacher_forced(case, steps, unfused, monkeypatch):
     args, buf, mac, learner, logger = build(case)
     o = OracleQLearner(case.agent_params, case.mixer_params, case.cfg())
     np.random.seed(case.sampler_seed)
+    rec = []
     for k in range(steps):
         batch = buf.sample(case.B)
         batch = batch[:, :batch.max_t_filled()]
@@ -166,18 +302,13 @@ def run_teacher_forced(case, steps, unfused, monkeypatch):
         fw = o.forward(nb)
         learner.train(batch, 1000 * k, case.episodes[k])
         st = learner.last_stats()
-        q = fw["mac_out"].copy()
-        q[nb["avail_actions"] == 0] = -9999999.0
-        top2 = -np.sort(-q[:, 1:], axis=3)[..., :2]
-        margin = top2[..., 0] - top2[..., 1]
-        clear = margin > MARGIN_EPS * np.maximum(1.0, np.abs(top2[..., 0]))
-        got = learner.last_cur_max_actions().cpu().numpy()
-        assert np.array_equal(got[clear], fw["cur_max_actions"][clear]), (name, k)
-        # fc1 relu decisions: the GPU's may differ only where the pre-activation is within RELU_EPS of 0
-        on_gpu = learner.last_intermediate(3).cpu().numpy() > 0
-        pre = fc1_preacts(o.p, nb["obs"], nb["actions_onehot"])
-        flip = on_gpu != (pre > 0)
-        assert np.all(np.abs(pre[flip]) <= RELU_EPS), (name, k, float(np.abs(pre[flip]).max()))
+        r, got, on_gpu = classify_decisions(learner, o, nb, fw)
+        r["step"] = k
+        rec.append(r)
+        # double-Q argmax exact wherever the top-2 margin > MARGIN_EPS * max(1, |Q|); relu decisions exact wherever
+        # |pre-activation| > RELU_EPS
+        assert r["dq_flips_outside_ties"] == 0, (name, k, r)
+        assert r["relu_flips_outside_ties"] == 0, (name, k, r)
         # on the near-ties the GPU may pick the other (equally valid in fp32 noise) branch: the oracle follows it
         st_o = o.train(nb, 1000 * k, case.episodes[k], cur_max_override=got, relu_override=on_gpu)
         for s_ in STATS:
@@ -194,6 +325,7 @@ def run_teacher_forced(case, steps, unfused, monkeypatch):
         assert rel(learner._sq.cpu().numpy(), sq_exp) < 1e-5, (name, k)
         assert rel(flat_params(learner), p_exp) < 1e-6, (name, k)
         assert np.abs(flat_params(learner) - o.flat("params")).max() <= 20 * 5e-4, (name, k)
+    write_record("teacher" + ("_unfused" if unfused else ""), name, rec)
 
 
 def test_data_parallel_norm_path_single_rank(cases):

@@ -141,6 +141,26 @@ def test_checkpoint_roundtrip(tmp_path):
     assert learner2.mac.agent.fc1.weight.data_ptr() == learner2._online.data_ptr()
 
 
+@pytest.mark.parametrize("name", ["tiny_qmix", "tiny_vdn"])
+def test_load_reference_checkpoint(golden_cases, name):
+    """agent.th / mixer.th / opt.th written by the REFERENCE's QLearner.save_models (q_learner.py:131-135) after
+    golden step 2 load with weights_only=True into the flat buffers: parameters bit-equal to the reference's, the
+    RMSprop square_avg and step count from opt.th."""
+    from tests.golden_utils import GOLDEN
+    from tests.gpu_helpers import CKPT, build
+    case = golden_cases[name]
+    args_, buf, mac, learner, logger = build(case, device="cpu")
+    path = os.path.join(GOLDEN, CKPT[name])
+    learner.load_models(path)
+    assert np.array_equal(learner._online[:learner.n_params].numpy(), case.z["step_params"][2])
+    sd = th.load(os.path.join(path, "opt.th"), weights_only=True)
+    sq = th.cat([sd["state"][i]["square_avg"].reshape(-1) for i in range(len(learner.params))])
+    assert th.equal(learner._sq, sq)
+    assert learner._opt_steps == 3 and float(learner.optimiser.state[learner.params[0]]["step"]) == 3
+    Pa = sum(p.numel() for p in mac.agent.parameters())
+    assert th.equal(learner._target[:Pa], learner._online[:Pa])   # target agent reloads agent.th (:138-140)
+
+
 def test_no_cpu_fallback():
     a, rb, mac, learner = build_cpu("vdn")
     rb.load_arrays({"filled": np.ones((4, 3, 1), dtype=np.int64)})

@@ -19,7 +19,7 @@ MARGIN_EPS = 1e-5
 TIGHT_STEPS = 12
 
 
-@pytest.mark.parametrize("name", ["tiny_qmix", "tiny_vdn", "tiny_qmix_full", "cfg2_qmix_ragged"])
+@pytest.mark.parametrize("name", ["tiny_qmix", "tiny_vdn", "tiny_qmix_full", "cfg2_qmix_ragged", "tiny_iql"])
 def test_intermediates_and_params(golden_cases, name):
     c = golden_cases[name]
     o = OracleQLearner(c.agent_params, c.mixer_params, c.cfg())
@@ -43,7 +43,8 @@ def test_intermediates_and_params(golden_cases, name):
     assert rel_err(o.flat("targets"), c.z["targets_final"]) < 5e-5
 
 
-@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_vdn", "cfg3_vdn", "cfg3_qmix", "cfg4_qmix"])
+@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_vdn", "cfg3_vdn", "cfg3_qmix", "cfg4_qmix", "cfg2_iql", "rw2_qmix",
+                                  "rw4_vdn", "wide_qmix", "cfg3_vdn_b128"])
 def test_cfg2_trajectory(golden_cases, name):
     c = golden_cases[name]
     o = OracleQLearner(c.agent_params, c.mixer_params, c.cfg())
