@@ -168,10 +168,11 @@ def build_coma_workload(cfg_name, device, n_episodes=1000, unique=128, seed=0, d
     return args, buf, learner, data, mac
 
 
-def rollout_baseline(cfg_name, device, budget_s=6.0):
-    """The rollout side (north_star: ParallelRunner stays on the host cores), timed on this host: EpisodeRunner on
-    the seeded FakeEnv at the config's shape (SC2 / SMAC cannot run offline), the HIP MAC step choosing actions,
-    episodes written straight into an HBM replay. One env process, batch_size_run = 1 (the episode runner)."""
+def rollout_baseline(cfg_name, device, budget_s=6.0, workers=8):
+    """The rollout side (north_star: ParallelRunner stays on the host cores), timed on this host: ParallelRunner with
+    `workers` env processes (batch_size_run = 8, qmix_smac.yaml) on the seeded FakeEnv at the config's shape
+    (SC2 / SMAC cannot run offline), the batched HIP MAC step choosing actions for every running env, each run's
+    batch written straight into an HBM replay."""
     import torch as th
     from pymarl_amd.components.episode_buffer import ReplayBuffer
     from pymarl_amd.components.transforms import OneHot
@@ -182,35 +183,39 @@ def rollout_baseline(cfg_name, device, budget_s=6.0):
     args = SN(n_agents=n, n_actions=A, state_shape=S, obs_shape=O, rnn_hidden_dim=64, obs_last_action=True,
               obs_agent_id=True, agent="rnn", mac="basic_mac", agent_output_type="q",
               action_selector="epsilon_greedy", epsilon_start=1.0, epsilon_finish=0.05, epsilon_anneal_time=50000,
-              batch_size_run=1, env="fake", env_args=dict(n_agents=n, n_actions=A, obs_dim=O, state_dim=S,
-                                                           episode_limit=T, seed=5),
-              device=str(device), use_cuda=True, test_nepisode=1, runner_log_interval=10 ** 9)
+              batch_size_run=workers, env="fake", env_args=dict(n_agents=n, n_actions=A, obs_dim=O, state_dim=S,
+                                                                 episode_limit=T, seed=5),
+              device=str(device), use_cuda=True, test_nepisode=workers, runner_log_interval=10 ** 9)
     logger = Logger(logging.getLogger("bench-rollout"))
-    runner = r_REGISTRY["episode"](args, logger)
-    scheme = {"state": {"vshape": S}, "obs": {"vshape": O, "group": "agents"},
-              "actions": {"vshape": (1,), "group": "agents", "dtype": th.long},
-              "avail_actions": {"vshape": (A,), "group": "agents", "dtype": th.int},
-              "reward": {"vshape": (1,)}, "terminated": {"vshape": (1,), "dtype": th.uint8}}
-    groups = {"agents": n}
-    preprocess = {"actions": ("actions_onehot", [OneHot(out_dim=A)])}
-    buf = ReplayBuffer(scheme, groups, 256, T + 1, preprocess=preprocess, device=device)
-    mac = mac_REGISTRY["basic_mac"](buf.scheme, groups, args)
-    mac.cuda()
-    runner.setup(scheme=scheme, groups=groups, preprocess=preprocess, mac=mac)
-    buf.insert_episode_batch(runner.run(test_mode=False))   # warm-up episode
-    th.cuda.synchronize()
-    steps, eps, t0 = 0, 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        b = runner.run(test_mode=False)
-        buf.insert_episode_batch(b)
-        steps += int(b["filled"].sum().item()) - 1
-        eps += 1
-    th.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "env steps/s", "cores": 1, "kind": "port",
-            "sample": f"{eps} EpisodeRunner episodes ({steps} env steps) on FakeEnv at {cfg_name}'s shape "
-                      f"(n={n}, A={A}, obs={O}, state={S}, limit={T}); SC2 unavailable offline; HIP MAC step, "
-                      f"HBM replay inserts; {dt / eps * 1e3:.1f} ms/episode"}
+    runner = r_REGISTRY["parallel"](args, logger)
+    try:
+        scheme = {"state": {"vshape": S}, "obs": {"vshape": O, "group": "agents"},
+                  "actions": {"vshape": (1,), "group": "agents", "dtype": th.long},
+                  "avail_actions": {"vshape": (A,), "group": "agents", "dtype": th.int},
+                  "reward": {"vshape": (1,)}, "terminated": {"vshape": (1,), "dtype": th.uint8}}
+        groups = {"agents": n}
+        preprocess = {"actions": ("actions_onehot", [OneHot(out_dim=A)])}
+        buf = ReplayBuffer(scheme, groups, 256, T + 1, preprocess=preprocess, device=device)
+        mac = mac_REGISTRY["basic_mac"](buf.scheme, groups, args)
+        mac.cuda()
+        runner.setup(scheme=scheme, groups=groups, preprocess=preprocess, mac=mac)
+        buf.insert_episode_batch(runner.run(test_mode=False))   # warm-up run
+        th.cuda.synchronize()
+        steps, eps, t0 = 0, 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s:
+            b = runner.run(test_mode=False)
+            buf.insert_episode_batch(b)
+            steps += int(b["filled"].sum().item()) - workers
+            eps += workers
+        th.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    finally:
+        runner.close_env()
+    return {"value": steps / dt, "unit": "env steps/s", "cores": workers, "kind": "port",
+            "sample": f"{eps} episodes ({steps} env steps) of ParallelRunner, {workers} env worker processes, on "
+                      f"FakeEnv at {cfg_name}'s shape (n={n}, A={A}, obs={O}, state={S}, limit={T}); SC2 unavailable "
+                      f"offline; batched HIP MAC step, HBM replay inserts; {dt / (eps / workers) * 1e3:.1f} ms per "
+                      f"{workers}-episode run"}
 
 
 def cpu_baseline(cfg_name, data, budget_s=12.0):

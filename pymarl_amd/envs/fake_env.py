@@ -3,7 +3,8 @@
 State and observations follow a seeded random walk that the joint action feeds back into, so a runner that records
 the wrong action or the wrong time slot produces a different episode. Action 1 is always available (as in the
 synthetic replay of pymarl_amd/utils/synthetic.py); an episode terminates at a seeded length in
-[episode_limit // 2, episode_limit], or is cut at the limit with info["episode_limit"] = True (episode_runner.py:69-78
+[episode_limit // 2, episode_limit] (or earlier, once the state crosses `end_threshold`, if given), or is cut at the
+limit with info["episode_limit"] = True (episode_runner.py:69-78
 turns that into terminated = False).
 """
 import numpy as np
@@ -13,7 +14,7 @@ from .multiagentenv import MultiAgentEnv
 
 class FakeEnv(MultiAgentEnv):
     def __init__(self, n_agents=3, n_actions=9, obs_dim=30, state_dim=48, episode_limit=60, seed=0, p_avail=0.7,
-                 p_truncate=0.5, **kwargs):
+                 p_truncate=0.5, end_threshold=None, **kwargs):
         self.n_agents = int(n_agents)
         self.n_actions = int(n_actions)
         self.obs_dim = int(obs_dim)
@@ -21,6 +22,9 @@ class FakeEnv(MultiAgentEnv):
         self.episode_limit = int(episode_limit)
         self.p_avail = float(p_avail)
         self.p_truncate = float(p_truncate)
+        # optional action-dependent early end: the episode also terminates once state[2] exceeds this (from t = 3),
+        # so identically seeded envs stepped with different actions end at different times
+        self.end_threshold = None if end_threshold is None else float(end_threshold)
         self._rng = np.random.Generator(np.random.PCG64(seed))
         self._proj = self._rng.standard_normal((self.n_agents * self.n_actions, self.state_dim)).astype(np.float32)
         self._obs_proj = self._rng.standard_normal((self.n_agents, self.state_dim, self.obs_dim)).astype(np.float32)
@@ -53,7 +57,8 @@ class FakeEnv(MultiAgentEnv):
         self._t += 1
         info = {}
         terminated = False
-        if self._t >= self._length:
+        early = self.end_threshold is not None and self._t >= 3 and self._state[2] > self.end_threshold
+        if self._t >= self._length or early:
             terminated = True
             info["battle_won"] = bool(self._state[1] > 0)
         elif self._t >= self.episode_limit:
@@ -97,3 +102,7 @@ class FakeEnv(MultiAgentEnv):
 
     def save_replay(self):
         pass
+
+    def get_stats(self):
+        """Env-side episode stats (SMAC's StarCraft2Env.get_stats; requested by the parallel runner)."""
+        return {}

@@ -1,3 +1,4 @@
 from .episode_runner import EpisodeRunner
+from .parallel_runner import ParallelRunner
 
-REGISTRY = {"episode": EpisodeRunner}
+REGISTRY = {"episode": EpisodeRunner, "parallel": ParallelRunner}

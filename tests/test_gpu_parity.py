@@ -97,10 +97,15 @@ def get_case(cases, name):
 
 
 def run_case(case, check_full, plan=None):
+    """Free run of the GPU learner against the reference's golden run (module doc). Beside it run two oracles: `o`
+    is reset to the GPU's state every step and classifies the GPU's decisions (near-ties, flips); the shadow `o2`
+    runs free from the same start but takes the GPU's decisions (allowed only where they are near-ties at its own
+    state), so GPU vs shadow measures the arithmetic alone, with the near-tie branch choices factored out."""
     from oracle.qlearner_np import OracleQLearner
     from tests.gpu_helpers import build, flat_grads, flat_params, flat_targets, rel
     args, buf, mac, learner, logger = build(case)
     o = OracleQLearner(case.agent_params, case.mixer_params, case.cfg())
+    o2 = OracleQLearner(case.agent_params, case.mixer_params, case.cfg())
     np.random.seed(case.sampler_seed)
     rec = []
     for k in range(case.steps):
@@ -111,22 +116,27 @@ def run_case(case, check_full, plan=None):
         nb, _ = case.batch(k)
         oracle_from_learner(o, case, learner)   # the oracle's decisions at the GPU's own state
         fw = o.forward(nb)
+        fw2 = o2.forward(nb)
         learner.train(batch, 1000 * k, case.episodes[k])
         if plan is not None and k == 0:
             got_plan = learner.last_plan()
             for key, v in plan.items():
                 assert got_plan[key] == v, (case.name, key, got_plan)
         st = learner.last_stats()
-        r, _, _ = classify_decisions(learner, o, nb, fw)
+        r, got, on_gpu = classify_decisions(learner, o, nb, fw)
+        r2, _, _ = classify_decisions(learner, o2, nb, fw2)
+        st2 = o2.train(nb, 1000 * k, case.episodes[k], cur_max_override=got, relu_override=on_gpu)
         r["step"] = k
         r["loss"] = st["loss"]
         r["ref_loss"] = float(case.z["stat_loss"][k])
+        r["shadow_loss"] = st2["loss"]
+        r["shadow_flips_outside_ties"] = r2["dq_flips_outside_ties"] + r2["relu_flips_outside_ties"]
         for s_ in STATS:
             ref = float(case.z["stat_" + s_][k])
             assert np.isfinite(st[s_]), (case.name, k, s_)
             r["rel_err_" + s_] = abs(st[s_] - ref) / max(abs(ref), 1e-12)
+            r["shadow_rel_err_" + s_] = abs(st[s_] - st2[s_]) / max(abs(st2[s_]), 1e-12)
         if "cur_max_actions" in case.z and k < case.z["cur_max_actions"].shape[0]:
-            got = learner.last_cur_max_actions().cpu().numpy()
             ref = case.z["cur_max_actions"][k].astype(np.int64)
             mo = learner.last_intermediate(0).cpu().numpy()[:, 1:max_t]
             mo = np.where(nb["avail_actions"][:, 1:] == 0, np.float32(-9999999.0), mo)
@@ -148,23 +158,34 @@ def run_case(case, check_full, plan=None):
     # every decision the GPU takes differently from the oracle at its own state is a near-tie
     for r in rec:
         assert r["dq_flips_outside_ties"] == 0 and r["relu_flips_outside_ties"] == 0, (case.name, r)
+    flip_steps = [r["step"] for r in rec if r["dq_flips"] + r["relu_flips"] > 0]
+    first_flip = flip_steps[0] if flip_steps else case.steps
+    # against the reference's recorded actions: exact on clear margins until a flip can have moved the parameters
+    for r in rec[:first_flip + 1]:
         assert r.get("ref_dq_mismatch_clear", 0) == 0, (case.name, r)
-    # the loss trajectory holds LOSS_RTOL for HOLD_STEPS steps, or up to a counted flip
+    # the loss trajectory holds LOSS_RTOL against the reference for HOLD_STEPS steps, or up to a counted flip
     errs = [r["rel_err_loss"] for r in rec]
     hold = next((k for k, e in enumerate(errs) if e > LOSS_RTOL), len(errs))
-    assert hold >= 1, (case.name, "step 0 loss", errs[0])
     for s_ in STATS:
-        assert rec[0]["rel_err_" + s_] <= LOSS_RTOL + 1e-6 / max(abs(float(case.z["stat_" + s_][0])), 1e-6), \
-            (case.name, s_, rec[0])
+        ref0 = abs(float(case.z["stat_" + s_][0]))
+        assert rec[0]["rel_err_" + s_] <= LOSS_RTOL + 1e-6 / max(ref0, 1e-6), (case.name, s_, rec[0])
     if hold < min(HOLD_STEPS, case.steps):
-        flips = [r["dq_flips"] + r["relu_flips"] + r.get("ref_dq_mismatch_ties", 0) for r in rec[:hold + 1]]
-        assert any(flips), (case.name, "loss left 1e-4 at step {} with no counted flip before it".format(hold), errs)
+        assert first_flip <= hold, (case.name, "loss left 1e-4 at step {} before any counted flip".format(hold), errs)
+    # with the GPU's near-tie choices factored out (shadow oracle), the loss holds LOSS_RTOL as long as the oracle
+    # holds the reference's own trajectory (HOLD_STEPS) and the shadow's decisions stay clear of forced flips
+    for r in rec[:HOLD_STEPS]:
+        if r["shadow_flips_outside_ties"]:
+            break
+        assert r["shadow_rel_err_loss"] <= LOSS_RTOL, (case.name, r["step"], [x["shadow_rel_err_loss"] for x in rec])
     for k in range(hold, case.steps):   # a different valid trajectory after a near-tie flip: sanity bound only
         ref = case.z["stat_loss"][k]
         assert 0.5 * ref <= rec[k]["loss"] <= 2.0 * ref, (case.name, k, errs)
     if "targets_final" in case.z:
-        tol = 1e-4 if hold >= case.steps else 2e-1
-        assert rel(flat_targets(learner), case.z["targets_final"]) < tol
+        # RMSprop's per-element 1/(sqrt(v)+eps) turns fp32 noise in a cancelling (near-zero) gradient element into
+        # an O(lr) step difference, so parameters agree per element only to an O(lr) band per step taken
+        # (the loss above, a global statistic, is the tight check)
+        d = np.abs(flat_targets(learner).astype(np.float64) - case.z["targets_final"])
+        assert d.max() <= 20 * 5e-4 * case.steps, (case.name, float(d.max()))
     if "sqavg_final" in case.z:
         assert rel(learner._sq.cpu().numpy(), case.z["sqavg_final"]) < 1e-4
     return learner

@@ -1,4 +1,5 @@
-"""The rollout side on the GPU: EpisodeRunner (FakeEnv) -> HBM ReplayBuffer -> QLearner.train,
+"""The rollout side on the GPU: EpisodeRunner or ParallelRunner (FakeEnv; 4 worker processes)
+-> HBM ReplayBuffer -> QLearner.train,
 with the HIP MAC step choosing the actions. Checks that the greedy (test-mode) actions the runner recorded are the
 oracle's masked argmax of the agent's Q on the recorded episode (clear margins; basic_controller.py:30-38,
 action_selectors.py:44-62), that every episode obeys the replay contract, and that training on runner-made episodes
@@ -15,7 +16,7 @@ pytestmark = pytest.mark.gpu
 N, A, O, S, LIMIT = 3, 9, 30, 48, 24
 
 
-def build():
+def build(kind="episode", bsr=1):
     from pymarl_amd.components.episode_buffer import ReplayBuffer
     from pymarl_amd.components.transforms import OneHot
     from pymarl_amd.controllers import REGISTRY as mac_REGISTRY
@@ -26,11 +27,12 @@ def build():
               mixer="qmix", lr=5e-4, optim_alpha=0.99, optim_eps=1e-5, grad_norm_clip=10.0, gamma=0.99, double_q=True,
               target_update_interval=200, learner_log_interval=0, obs_last_action=True, obs_agent_id=True,
               agent="rnn", mac="basic_mac", agent_output_type="q", action_selector="epsilon_greedy",
-              epsilon_start=1.0, epsilon_finish=0.05, epsilon_anneal_time=500, batch_size=8, batch_size_run=1,
-              env="fake", env_args=dict(n_agents=N, n_actions=A, obs_dim=O, state_dim=S, episode_limit=LIMIT, seed=4),
+              epsilon_start=1.0, epsilon_finish=0.05, epsilon_anneal_time=500, batch_size=8, batch_size_run=bsr,
+              env="fake", env_args=dict(n_agents=N, n_actions=A, obs_dim=O, state_dim=S, episode_limit=LIMIT, seed=4,
+                                        end_threshold=None if kind == "episode" else -0.9),
               device="cuda", use_cuda=True, test_nepisode=1, runner_log_interval=10 ** 9, learner="q_learner")
     logger = Logger(logging.getLogger("runner-test"))
-    runner = r_REGISTRY["episode"](args, logger)
+    runner = r_REGISTRY[kind](args, logger)
     scheme = {"state": {"vshape": S}, "obs": {"vshape": O, "group": "agents"},
               "actions": {"vshape": (1,), "group": "agents", "dtype": th.long},
               "avail_actions": {"vshape": (A,), "group": "agents", "dtype": th.int},
@@ -45,42 +47,48 @@ def build():
     return args, runner, buf, mac, learner
 
 
-def check_contract(b):
-    filled = b["filled"][0, :, 0].cpu().numpy()
-    term = b["terminated"][0, :, 0].cpu().numpy()
+def check_contract(b, i=0):
+    filled = b["filled"][i, :, 0].cpu().numpy()
+    term = b["terminated"][i, :, 0].cpu().numpy()
     L = int(filled.sum()) - 1
     assert np.all(filled[:L + 1] == 1) and np.all(filled[L + 1:] == 0)
     assert term[L:].sum() == 0 and term[:max(0, L - 1)].sum() == 0
     assert L == LIMIT or term[L - 1] == 1   # cut at the limit, or a true termination at L-1
-    av = b["avail_actions"][0, :L + 1].cpu().numpy()
-    act = b["actions"][0, :L + 1, :, 0].cpu().numpy()
+    av = b["avail_actions"][i, :L + 1].cpu().numpy()
+    act = b["actions"][i, :L + 1, :, 0].cpu().numpy()
     assert np.all(np.take_along_axis(av, act[..., None], 2) == 1)
     return L
 
 
-def test_runner_greedy_actions_and_training():
+@pytest.mark.parametrize("kind,bsr", [("episode", 1), ("parallel", 4)])
+def test_runner_greedy_actions_and_training(kind, bsr):
     from oracle.qlearner_np import agent_unroll
-    args, runner, buf, mac, learner = build()
+    args, runner, buf, mac, learner = build(kind, bsr)
     np.random.seed(0)
     th.manual_seed(0)
-    for ep in range(10):
-        b = runner.run(test_mode=False)
-        check_contract(b)
-        buf.insert_episode_batch(b)
-    # greedy test-mode episode: recorded actions = masked argmax of the agent's Q (clear margins)
-    b = runner.run(test_mode=True)
-    L = check_contract(b)
+    try:
+        for ep in range(10 // bsr):
+            b = runner.run(test_mode=False)
+            for i in range(bsr):
+                check_contract(b, i)
+            buf.insert_episode_batch(b)
+        # greedy test-mode episodes: recorded actions = masked argmax of the agent's Q (clear margins)
+        b = runner.run(test_mode=True)
+    finally:
+        runner.close_env()
     p = {k: v.detach().cpu().numpy() for k, v in mac.agent.state_dict().items()}
-    obs = b["obs"][:, :L + 1].cpu().numpy()
-    oh = b["actions_onehot"][:, :L + 1].cpu().numpy()
-    q, _ = agent_unroll(p, obs, oh)
-    av = b["avail_actions"][:, :L + 1].cpu().numpy()
-    qm = np.where(av == 0, -np.inf, q)
-    greedy = qm.argmax(-1)
-    top2 = -np.sort(-qm, -1)[..., :2]
-    clear = (top2[..., 0] - top2[..., 1]) > 1e-4
-    rec = b["actions"][:, :L + 1, :, 0].cpu().numpy()
-    assert np.array_equal(rec[clear], greedy[clear])
+    for i in range(bsr):
+        L = check_contract(b, i)
+        obs = b["obs"][i:i + 1, :L + 1].cpu().numpy()
+        oh = b["actions_onehot"][i:i + 1, :L + 1].cpu().numpy()
+        q, _ = agent_unroll(p, obs, oh)
+        av = b["avail_actions"][i:i + 1, :L + 1].cpu().numpy()
+        qm = np.where(av == 0, -np.inf, q)
+        greedy = qm.argmax(-1)
+        top2 = -np.sort(-qm, -1)[..., :2]
+        clear = (top2[..., 0] - top2[..., 1]) > 1e-4
+        rec = b["actions"][i:i + 1, :L + 1, :, 0].cpu().numpy()
+        assert np.array_equal(rec[clear], greedy[clear])
     # training on runner-made episodes
     for k in range(3):
         s = buf.sample(8)

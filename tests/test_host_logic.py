@@ -166,3 +166,25 @@ def test_no_cpu_fallback():
     rb.load_arrays({"filled": np.ones((4, 3, 1), dtype=np.int64)})
     with pytest.raises(_lib.MQError, match="no CPU"):
         learner.train(rb.sample(3), 0, 0)
+
+
+def test_logger_interface():
+    """utils/logging.py keeps the reference's Logger contract: history, sacred sink, recent-stats printing."""
+    lines = []
+    console = SN(info=lines.append)
+    lg = Logger(console)
+    assert not lg.use_tb and not lg.use_sacred
+    run = SN(info={})
+    lg.setup_sacred(run)
+    for t in range(7):
+        lg.log_stat("loss", float(t), t)
+        lg.log_stat("epsilon", 1.0 - 0.1 * t, t)
+    lg.log_stat("episode", 12, 6)
+    lg.log_stat("hidden", 1.0, 6, to_sacred=False)
+    assert lg.use_sacred and run.info["loss"] == [float(t) for t in range(7)] and run.info["loss_T"] == list(range(7))
+    assert "hidden" not in run.info
+    assert lg.stats["loss"][-1] == (6, 6.0)
+    assert lg.recent("loss") == np.mean([2, 3, 4, 5, 6]) and abs(lg.recent("epsilon") - 0.4) < 1e-12
+    lg.print_recent_stats()
+    assert lines[-1].startswith("Recent Stats | t_env:          6 | Episode:       12\n")
+    assert "loss:" in lines[-1] and "4.0000" in lines[-1]

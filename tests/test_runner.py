@@ -72,9 +72,11 @@ def test_episode_runner_matches_reference():
             assert np.array_equal(got, ref), (e, k)
     assert runner.t_env == int(z["t_env"])
     names = list(z["stat_names"])
-    ref_stats = [(names[int(i)], v, int(t)) for i, v, t in z["stats"]]
-    assert [(k, t) for k, _, t in logger.stats] == [(k, t) for k, _, t in ref_stats]
-    for (k, v, _), (_, rv, _) in zip(logger.stats, ref_stats):
+    # compared as sorted (key, t) lists: the reference orders the per-key "_mean" stats by a Python set
+    ref_stats = sorted((names[int(i)], int(t), v) for i, v, t in z["stats"])
+    got_stats = sorted((k, t, v) for k, v, t in logger.stats)
+    assert [(k, t) for k, t, _ in got_stats] == [(k, t) for k, t, _ in ref_stats]
+    for (k, _, v), (_, _, rv) in zip(got_stats, ref_stats):
         assert abs(v - rv) <= 1e-6 * max(1.0, abs(rv)), (k, v, rv)
 
 
