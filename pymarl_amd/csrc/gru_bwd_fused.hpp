@@ -40,15 +40,20 @@ inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_
 
 // VAR: ablation bits (production = 0): 4 producers do no MFMA work, 8 per-phase cycle bins of the chain
 // (scripts/rec_micro.hip), 128 chain waves at s_setprio 2, 256 the chain's inputs loaded two steps ahead,
-// 512 the X1 / XIN rows of the next chunk loaded one chunk ahead.
+// 512 the X1 / XIN rows of the next chunk loaded one chunk ahead, 1024 SIMD-split roles: the chain runs in waves
+// 0, 1, 4, 5 and the producers in waves 2, 3, 6, 7. Waves w and w + 4 of a 512-thread workgroup share a SIMD, so
+// the chain then owns two SIMDs outright and the producers' f32 MFMAs (which hold the SIMD's FMA datapath) run on
+// the other two instead of beside every chain wave.
 template <int VAR = 0>
 __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
                                                             Work w, int64_t slab_len, int64_t slab1_len) {
   __shared__ BwdFusedLds S;
   extern __shared__ float dyn[];   // W2 [A][H] | dW2 partial [A][H] | db2 [A]
   const int tid = threadIdx.x;
-  const bool chain = tid < 256;
-  const int lt = tid & 255, k = lt >> 2, q = lt & 3;
+  constexpr bool kSplit = (VAR & 1024) != 0;
+  const bool chain = kSplit ? ((tid >> 7) & 1) == 0 : tid < 256;
+  // role-local thread id 0..255 (wave-uniform role; lanes of a quad stay in one wave)
+  const int lt = kSplit ? ((tid & 127) | ((tid >> 8) << 7)) : (tid & 255), k = lt >> 2, q = lt & 3;
   const int R = d.R, A = d.A, T = d.T, Tp = d.Tp, I = d.I;
   const int cl = (Tp - 1) / FCH;
   const int r = blockIdx.x;
@@ -209,7 +214,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     if (q < 3) { slab[o_bi + q * H + k] = db_i; slab[o_bh + q * H + k] = db_h; }
   } else {
     // ================================================================== producer waves
-    const int ptid = tid - 256, wv = ptid >> 6, lane = ptid & 63, g = lane >> 4, c16 = lane & 15;
+    const int ptid = kSplit ? lt : tid - 256, wv = ptid >> 6, lane = ptid & 63, g = lane >> 4, c16 = lane & 15;
     const int Kq = (I + 15) / 16 * 4;
     f32x4 acc_hh[3][4], acc_ih[3][4], acc_w1[7];
 #pragma unroll
@@ -416,6 +421,8 @@ inline void launch_bwd_fused(dim3 grid, size_t dyn, hipStream_t s, const Dims& d
     hipLaunchKernelGGL(gru_bwd_fused_kernel<768>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
   else if (var == 384)
     hipLaunchKernelGGL(gru_bwd_fused_kernel<384>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else if (var == 1792)
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<1792>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
   else
     hipLaunchKernelGGL(gru_bwd_fused_kernel<0>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
 }
