@@ -11,6 +11,7 @@
  *                      BasicMAC.forward's pi_logits branch src/controllers/basic_controller.py:53-73
  *   mc_update_targets  COMALearner._update_targets                       src/learners/coma_learner.py:150-152
  *   mc_policy          BasicMAC.forward pi_logits post-processing        src/controllers/basic_controller.py:53-73
+ *   mc_critic_forward  COMACritic.forward(batch, t=None)                 src/modules/critics/coma.py:22-58
  *   mc_copy_intermediate  (test hook) the critic's per-step Q values, the TD(lambda) targets, the policy
  *   mc_set_data_parallel  no reference counterpart: data-parallel COMA ("COMA caveat")
  */
@@ -61,6 +62,12 @@ int mc_update_targets(mc_handle* h, void* stream);
  * unless test_mode the epsilon floor (+ zeroing when mask_before_softmax). avail [rows][n_actions] int32. */
 int mc_policy(float* logits, const int32_t* avail, int32_t rows, int32_t n_actions, float epsilon,
               int32_t mask_before_softmax, int32_t test_mode, void* stream);
+/* COMACritic.forward(batch, t) outside train(): critic = fc1.weight .. fc3.bias (MC_P_* order); t < 0 means
+ * every stored step of the batch (t=None), else the single step t. q_out [batch_size][Tq][n_agents][n_actions],
+ * Tq = t_len or 1; workspace: mc_critic_forward_workspace(cfg, batch_size, Tq) floats of device memory. */
+int64_t mc_critic_forward_workspace(const mc_config* cfg, int32_t batch_size, int32_t t_count);
+int mc_critic_forward(const float* critic, const mc_config* cfg, const mq_replay* batch, int32_t t, float* q_out,
+                      float* workspace, void* stream);
 /* Optional HIP-event timing of train steps (bench / profiling): on != 0 records events around the critic's
  * target pass + TD(lambda), the T-step critic chain, and the actor part of every following mc_train_step;
  * mc_phase_times writes the last step's [prologue, critic chain, actor] ms (synchronises on the events). */

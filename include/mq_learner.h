@@ -16,6 +16,7 @@
  *   mq_mac_forward       BasicMAC.forward(ep_batch, t)                   src/controllers/basic_controller.py:40-75
  *   mq_agent_forward     RNNAgent.forward(inputs, hidden_state)          src/modules/agents/rnn_agent.py:27-36
  *   mq_greedy_actions    EpsilonGreedyActionSelector greedy branch      src/components/action_selectors.py:44-62
+ *   mq_qmix_forward      QMixer.forward(agent_qs, states)                src/modules/mixers/qmix.py:28-47
  *   mq_replay.ep_ids     ReplayBuffer.sample -> EpisodeBatch.__getitem__ gather, episode_buffer.py:165-217,291-298
  *                        (ids drawn on the host exactly as the reference does; the gather is fused into kernels)
  */
@@ -112,6 +113,12 @@ int mq_agent_forward(mq_handle* h, const float* inputs, int32_t rows, const floa
 /* argmax over available actions (unavailable = -inf, first index on ties) of q [rows][n_actions]. */
 int mq_greedy_actions(const float* q, const int32_t* avail, int64_t* out, int32_t rows, int32_t n_actions,
                       void* stream);
+
+/* QMixer.forward(agent_qs, states) outside train(): mixer = the mixer's parameters in QMixer.parameters() order
+ * (hyper_w_1.weight .. V.2.bias, the MQ_P_HW1_W .. MQ_P_V2_B block), agent_qs [rows][n_agents], states
+ * [rows][state_dim], q_tot [rows]. */
+int mq_qmix_forward(const float* mixer, int32_t n_agents, int32_t state_dim, int32_t embed_dim,
+                    const float* agent_qs, const float* states, float* q_tot, int32_t rows, void* stream);
 
 /* Which kernel variants the last mq_forward_backward launched (test / profiling introspection; no device sync).
  * rw_fwd / rw_bwd: rows per workgroup of the unfused recurrences (0 when the fused kernel ran). */

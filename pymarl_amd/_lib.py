@@ -26,10 +26,11 @@ EXPORTS = [
     "mq_last_error", "mq_create", "mq_destroy", "mq_param_offsets", "mq_bind", "mq_forward_backward", "mq_apply",
     "mq_train_step", "mq_update_targets", "mq_copy_intermediate", "mq_mac_forward", "mq_agent_forward",
     "mq_greedy_actions", "mq_set_timing", "mq_phase_times", "mq_phase_names", "mq_set_data_parallel",
-    "mq_last_plan",
+    "mq_last_plan", "mq_qmix_forward",
     # include/mc_coma.h
     "mc_create", "mc_destroy", "mc_param_offsets", "mc_bind", "mc_train_step", "mc_update_targets", "mc_policy",
-    "mc_copy_intermediate", "mc_set_timing", "mc_phase_times", "mc_set_data_parallel",
+    "mc_copy_intermediate", "mc_set_timing", "mc_phase_times", "mc_set_data_parallel", "mc_critic_forward",
+    "mc_critic_forward_workspace",
 ]
 
 # mc_allreduce_fn (include/mc_coma.h): int (*)(float* buf, int64_t count, void* stream, void* ctx)
@@ -125,6 +126,9 @@ def load(required=True):
         "mq_set_timing": ([vp, i32, ctypes.c_uint32], ctypes.c_int),
         "mq_set_data_parallel": ([vp, i32], ctypes.c_int),
         "mq_last_plan": ([vp, ctypes.POINTER(MQPlan)], ctypes.c_int),
+        "mq_qmix_forward": ([vp, i32, i32, i32, vp, vp, vp, i32, vp], ctypes.c_int),
+        "mc_critic_forward_workspace": ([ctypes.POINTER(MCConfig), i32, i32], i64),
+        "mc_critic_forward": ([vp, ctypes.POINTER(MCConfig), ctypes.POINTER(MQReplay), i32, vp, vp, vp], ctypes.c_int),
         "mq_phase_times": ([vp, ctypes.POINTER(ctypes.c_float), i32, ctypes.POINTER(i32)], ctypes.c_int),
         "mc_create": ([ctypes.POINTER(MCConfig), ctypes.POINTER(vp)], ctypes.c_int),
         "mc_destroy": ([vp], ctypes.c_int),

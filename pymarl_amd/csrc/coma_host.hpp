@@ -64,6 +64,58 @@ int mc_agent_config(const mc_config& c, mq_config* a) {
 
 extern "C" {
 
+int64_t mc_critic_forward_workspace(const mc_config* cfg, int32_t batch_size, int32_t t_count) {
+  if (!cfg || batch_size < 1 || t_count < 1) return -1;
+  const int n = cfg->n_agents, A = cfg->n_actions;
+  const int64_t Kp = ((int64_t)cfg->state_dim + cfg->obs_dim + 2 * n * A + n + 3) & ~int64_t(3);
+  const int64_t M = (int64_t)t_count * batch_size * n;
+  return align_up(M * Kp) + 2 * align_up(M * CH) + align_up(M * A);
+}
+
+int mc_critic_forward(const float* critic, const mc_config* cfg, const mq_replay* batch, int32_t t, float* q_out,
+                      float* workspace, void* stream) {
+  if (!critic || !cfg || !batch || !q_out || !workspace) return set_err(MQ_ERR_ARG, "mc_critic_forward: NULL pointer");
+  if (!batch->obs || !batch->state || !batch->actions || !batch->filled)
+    return set_err(MQ_ERR_ARG, "mc_critic_forward: batch needs obs, state, actions and filled");
+  if (batch->batch_size < 1 || batch->t_len < 1 || batch->t_len > batch->t_stride)
+    return set_err(MQ_ERR_ARG, "mc_critic_forward: bad batch dimensions");
+  if (t >= batch->t_len) return set_err(MQ_ERR_ARG, "mc_critic_forward: t outside the batch");
+  if (batch->ep_ids_host && batch->batch_size > MQ_INLINE_IDS && !batch->ep_ids)
+    return set_err(MQ_ERR_ARG, "mc_critic_forward: more than MQ_INLINE_IDS episodes need device ids");
+  hipStream_t s = (hipStream_t)stream;
+  const int n = cfg->n_agents, A = cfg->n_actions, B = batch->batch_size, R = B * n;
+  const int Tq = t < 0 ? batch->t_len : 1, t0 = t < 0 ? 0 : t;
+  CDims cd{};
+  cd.n = n; cd.A = A; cd.O = cfg->obs_dim; cd.S = cfg->state_dim;
+  cd.Kc = cfg->state_dim + cfg->obs_dim + 2 * n * A + n;
+  cd.Kp = (cd.Kc + 3) & ~3;
+  cd.R = R; cd.B = B; cd.Tp = batch->t_len; cd.T = batch->t_len - 1; cd.t_stride = batch->t_stride;
+  cd.dR = make_fastdiv((uint32_t)R);
+  cd.dN = make_fastdiv((uint32_t)n);
+  const Rep rp = make_rep(batch);
+  const int64_t M = (int64_t)Tq * R;
+  float* X = workspace;
+  float* H1 = X + align_up(M * cd.Kp);
+  float* H2 = H1 + align_up(M * CH);
+  float* Q = H2 + align_up(M * CH);
+  // offsets of fc1.weight .. fc3.bias (MC_P_* order)
+  const int64_t o_w1 = 0, o_b1 = (int64_t)CH * cd.Kc, o_w2 = o_b1 + CH, o_b2 = o_w2 + (int64_t)CH * CH,
+                o_w3 = o_b2 + CH, o_b3 = o_w3 + (int64_t)A * CH;
+  hipLaunchKernelGGL(coma_xin_kernel, dim3((unsigned)M), dim3(256), 0, s, cd, rp, X, t0);
+  MQ_HIP(hipGetLastError());
+  CLinProb l1{X, cd.Kp, critic + o_w1, critic + o_b1, H1, M, CH, cd.Kc, 1};
+  MQ_HIP(launch_gemm(l1, (int)M, CH, 1, s));
+  CLinProb l2{H1, CH, critic + o_w2, critic + o_b2, H2, M, CH, CH, 1};
+  MQ_HIP(launch_gemm(l2, (int)M, CH, 1, s));
+  CLinProb l3{H2, CH, critic + o_w3, critic + o_b3, Q, M, A, CH, 0};
+  MQ_HIP(launch_gemm(l3, (int)M, A, 1, s));
+  const int64_t tot = M * A;
+  hipLaunchKernelGGL(coma_q_layout_kernel, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, 4096)), dim3(256), 0, s,
+                     (const float*)Q, q_out, Tq, B, n, A);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
 int mc_create(const mc_config* cfg, mc_handle** out) {
   if (!cfg || !out) return set_err(MQ_ERR_ARG, "NULL argument");
   const mc_config& c = *cfg;

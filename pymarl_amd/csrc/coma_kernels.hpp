@@ -54,9 +54,10 @@ MQ_DEV float coma_mask(const Rep& rp, int64_t slot, int t) {
 // state | obs | actions_onehot[t] of every agent with the row's own block zeroed | actions_onehot[t-1] (0 at t = 0)
 // | onehot(agent) | zero padding to Kp. actions_onehot is the reference's OneHot transform of the stored action,
 // zero on unfilled slots (the runner never writes them).
-__global__ __launch_bounds__(256) void coma_xin_kernel(CDims d, Rep rp, float* __restrict__ X) {
+// t0: first stored step (the standalone COMACritic.forward(batch, t) builds one step's rows, coma.py:40-45).
+__global__ __launch_bounds__(256) void coma_xin_kernel(CDims d, Rep rp, float* __restrict__ X, int t0 = 0) {
   const int tr = blockIdx.x;
-  const int t = (int)fdiv((uint32_t)tr, d.dR), r = tr - t * d.R;
+  const int tl = (int)fdiv((uint32_t)tr, d.dR), r = tr - tl * d.R, t = t0 + tl;
   const int b = (int)fdiv((uint32_t)r, d.dN), ag = r - b * d.n;
   const int64_t slot = rp.ep(b) * d.t_stride + t;
   const float* st = rp.state + slot * d.S;

@@ -43,7 +43,9 @@ inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_
 // 512 the X1 / XIN rows of the next chunk loaded one chunk ahead, 1024 SIMD-split roles: the chain runs in waves
 // 0, 1, 4, 5 and the producers in waves 2, 3, 6, 7. Waves w and w + 4 of a 512-thread workgroup share a SIMD, so
 // the chain then owns two SIMDs outright and the producers' f32 MFMAs (which hold the SIMD's FMA datapath) run on
-// the other two instead of beside every chain wave.
+// the other two instead of beside every chain wave (measured slower: the producers, two per SIMD, then set the
+// step), 2048 the next step's W2 lookup issued at the top of the step with a 4-slot input rotation, 4096 four
+// accumulator pairs in the W_hh^T mat-vec.
 template <int VAR = 0>
 __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
                                                             Work w, int64_t slab_len, int64_t slab1_len) {
@@ -51,6 +53,8 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
   extern __shared__ float dyn[];   // W2 [A][H] | dW2 partial [A][H] | db2 [A]
   const int tid = threadIdx.x;
   constexpr bool kSplit = (VAR & 1024) != 0;
+  constexpr bool kEarlyW2 = (VAR & 2048) != 0;
+  constexpr bool kAcc4 = (VAR & 4096) != 0;
   const bool chain = kSplit ? ((tid >> 7) & 1) == 0 : tid < 256;
   // role-local thread id 0..255 (wave-uniform role; lanes of a quad stay in one wave)
   const int lt = kSplit ? ((tid & 127) | ((tid >> 8) << 7)) : (tid & 255), k = lt >> 2, q = lt & 3;
@@ -130,6 +134,9 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     // load has two chain steps of latency instead of one); nxt: the next step's slot, whose w2 is looked up here
     auto step = [&](int t, const In& cur, In& nxt, In& ahead, int dist) {
       load(t - dist, ahead);
+      // VAR 2048: the next step's W2[a][k] lookup is issued here, a whole step before its use, instead of at the
+      // end of the step where its LDS latency sat on the dh chain (nxt was loaded two steps ago: 4-slot rotation)
+      if (kEarlyW2) lookup_w2(nxt);
       const int p = t & (FCH - 1), cb = (t / FCH) & 1;
       const float gr = quad_bcast<0>(cur.g), gz = quad_bcast<1>(cur.g), gn = quad_bcast<2>(cur.g),
                   ghn = quad_bcast<3>(cur.g);
@@ -152,19 +159,33 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       lds_barrier();
       // dh_{t-1} = dh * z + W_hh^T dgh
       const f32x4* dg4 = (const f32x4*)(&S.gh[cb][p][48 * q]);
-      f32x2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
+      if (kAcc4) {   // VAR 4096: four accumulator pairs, dependency chains of 6 instead of 12
+        f32x2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f}, a2 = {0.0f, 0.0f}, a3 = {0.0f, 0.0f};
 #pragma unroll
-      for (int c4 = 0; c4 < 12; ++c4) {
-        const f32x4 dg = dg4[c4];
-        a01 = pk_fma(wT[2 * c4], f32x2{dg[0], dg[1]}, a01);
-        a23 = pk_fma(wT[2 * c4 + 1], f32x2{dg[2], dg[3]}, a23);
+        for (int c4 = 0; c4 < 12; c4 += 2) {
+          const f32x4 dg = dg4[c4], dh4 = dg4[c4 + 1];
+          a0 = pk_fma(wT[2 * c4], f32x2{dg[0], dg[1]}, a0);
+          a1 = pk_fma(wT[2 * c4 + 1], f32x2{dg[2], dg[3]}, a1);
+          a2 = pk_fma(wT[2 * c4 + 2], f32x2{dh4[0], dh4[1]}, a2);
+          a3 = pk_fma(wT[2 * c4 + 3], f32x2{dh4[2], dh4[3]}, a3);
+        }
+        carry = cz + quad_sum(((a0.x + a0.y) + (a1.x + a1.y)) + ((a2.x + a2.y) + (a3.x + a3.y)));
+      } else {
+        f32x2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
+#pragma unroll
+        for (int c4 = 0; c4 < 12; ++c4) {
+          const f32x4 dg = dg4[c4];
+          a01 = pk_fma(wT[2 * c4], f32x2{dg[0], dg[1]}, a01);
+          a23 = pk_fma(wT[2 * c4 + 1], f32x2{dg[2], dg[3]}, a23);
+        }
+        carry = cz + quad_sum((a01.x + a01.y) + (a23.x + a23.y));
       }
-      carry = cz + quad_sum((a01.x + a01.y) + (a23.x + a23.y));
-      lookup_w2(nxt);
+      if (!kEarlyW2) lookup_w2(nxt);
     };
-    In sa, sb, sc;
+    In sa, sb, sc, sd;
     load(Tp - 1, sa);
-    if (VAR & 256) load(Tp - 2, sb);
+    if (VAR & (256 | 2048)) load(Tp - 2, sb);
+    if (kEarlyW2) load(Tp - 3, sc);
     drain_vmem();
     lds_barrier();
     lookup_w2(sa);
@@ -193,6 +214,16 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
         for (int i = 0; i < FCH; ++i) st[i] = bins[i];
         st[16] = __builtin_amdgcn_s_memtime() - c0;
       }
+    } else if (kEarlyW2) {   // 4-slot rotation: inputs loaded three steps ahead
+      for (; t - 3 >= 0; t -= 4) {
+        step(t, sa, sb, sd, 3);
+        step(t - 1, sb, sc, sa, 3);
+        step(t - 2, sc, sd, sb, 3);
+        step(t - 3, sd, sa, sc, 3);
+      }
+      if (t >= 0) step(t, sa, sb, sd, 3);
+      if (t - 1 >= 0) step(t - 1, sb, sc, sa, 3);
+      if (t - 2 >= 0) step(t - 2, sc, sd, sb, 3);
     } else if (VAR & 256) {
       for (; t - 2 >= 0; t -= 3) {
         step(t, sa, sb, sc, 2);
@@ -423,6 +454,16 @@ inline void launch_bwd_fused(dim3 grid, size_t dyn, hipStream_t s, const Dims& d
     hipLaunchKernelGGL(gru_bwd_fused_kernel<384>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
   else if (var == 1792)
     hipLaunchKernelGGL(gru_bwd_fused_kernel<1792>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else if (var == 2816)
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<2816>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else if (var == 4864)
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<4864>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else if (var == 6912)
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<6912>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else if (var == 772)   // diagnostic (wrong gradients): producers idle, the chain alone
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<772>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else if (var == 1796)  // diagnostic (wrong gradients): SIMD-split chain alone
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<1796>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
   else
     hipLaunchKernelGGL(gru_bwd_fused_kernel<0>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
 }

@@ -30,6 +30,7 @@
 #include "hyper_kernel.hpp"
 #include "dwh_kernel.hpp"
 #include "optim_kernels.hpp"
+#include "module_fwd.hpp"
 
 using namespace mq;
 
@@ -690,6 +691,21 @@ int mq_greedy_actions(const float* q, const int32_t* avail, int64_t* out, int32_
   if (rows == 0) return MQ_OK;
   hipLaunchKernelGGL(greedy_kernel, dim3((rows + 255) / 256), dim3(256), 0, (hipStream_t)stream, q, avail, out,
                      (int)rows, (int)n_actions);
+  MQ_HIP(hipGetLastError());
+  return MQ_OK;
+}
+
+int mq_qmix_forward(const float* mixer, int32_t n_agents, int32_t state_dim, int32_t embed_dim,
+                    const float* agent_qs, const float* states, float* q_tot, int32_t rows, void* stream) {
+  if (!mixer || !agent_qs || !states || !q_tot || rows < 0) return set_err(MQ_ERR_ARG, "bad mq_qmix_forward args");
+  if (n_agents < 1 || n_agents > 64 || embed_dim < 1 || embed_dim > 64 || state_dim < 1)
+    return set_err(MQ_ERR_ARG, "mq_qmix_forward: n_agents / embed_dim in [1, 64], state_dim >= 1");
+  if (rows == 0) return MQ_OK;
+  const size_t lds = qmix_forward_lds(n_agents, state_dim, embed_dim);
+  if (lds > 160 * 1024) return set_err(MQ_ERR_ARG, "mq_qmix_forward: state_dim too large for the LDS staging");
+  hipLaunchKernelGGL(qmix_forward_kernel, dim3((rows + QMF_ROWS - 1) / QMF_ROWS), dim3(256), lds,
+                     (hipStream_t)stream, mixer, (int)n_agents, (int)state_dim, (int)embed_dim, agent_qs, states,
+                     q_tot, (int)rows);
   MQ_HIP(hipGetLastError());
   return MQ_OK;
 }

@@ -231,9 +231,15 @@ int main(int argc, char** argv) {
       std::sort(a.begin(), a.end()); std::sort(b.begin(), b.end());
       printf("fused bwd V0 median %.1f min %.1f | V128 median %.1f min %.1f\n", a[4], a[0], b[4], b[0]);
     }
+    printf("fused bwd V768 %.1f us | V772 (producers idle) %.1f | V1792 (SIMD split) %.1f | V1796 %.1f\n",
+           runbf(gru_bwd_fused_kernel<768>), runbf(gru_bwd_fused_kernel<772>), runbf(gru_bwd_fused_kernel<1792>),
+           runbf(gru_bwd_fused_kernel<1796>));
     CK(hipFree(w.slab_mix)); CK(hipMalloc(&w.slab_mix, 32 * 8 * d.R));
-    for (int var : {8, 12}) {
-      if (var == 8) runbf(gru_bwd_fused_kernel<8>); else runbf(gru_bwd_fused_kernel<12>);
+    for (int var : {776, 780, 1800, 1804}) {
+      if (var == 776) runbf(gru_bwd_fused_kernel<776>);
+      else if (var == 780) runbf(gru_bwd_fused_kernel<780>);
+      else if (var == 1800) runbf(gru_bwd_fused_kernel<1800>);
+      else runbf(gru_bwd_fused_kernel<1804>);
       std::vector<uint64_t> sb(32 * d.R);
       CK(hipMemcpy(sb.data(), w.slab_mix, sb.size() * 8, hipMemcpyDeviceToHost));
       double tot = 0; for (int i = 0; i < d.R; ++i) tot += sb[32 * i + 16];

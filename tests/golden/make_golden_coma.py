@@ -143,6 +143,12 @@ def run_case(name, case):
         eps = float(learner.mac.action_selector.schedule.eval(t_env))
         learner.mac.action_selector.epsilon = eps
         eps_all.append(eps)
+        if case["full"] and k == 0:
+            # the reference COMACritic.forward (coma.py:22-27) on its own, all steps and single steps
+            with th.no_grad():
+                out["step0_critic_q_all"] = learner.critic(batch).numpy().copy()
+                out["step0_critic_q_t0"] = learner.critic(batch, t=0).numpy().copy()
+                out["step0_critic_q_t2"] = learner.critic(batch, t=2).numpy().copy()
         learner.train(batch, t_env=t_env, episode_num=8 * k)
         if case["full"]:
             if k == 0:
