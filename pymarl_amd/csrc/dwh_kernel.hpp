@@ -21,6 +21,7 @@
 // Each wave walks the same m steps in the same order in both, so their results are bitwise equal.
 #pragma once
 #include "learner_gemms.hpp"
+#include "optim_kernels.hpp"
 
 namespace mq {
 
@@ -30,13 +31,13 @@ constexpr int DWH_T = 32;   // output tile edge
 // VAR (scripts/rec_micro.hip only): 1 no MFMA, 2 no operand loads. U: MFMAs (2 m-rows each) per pipelined block.
 template <int VAR, int U>
 MQ_DEV void dwh_body(Dims d, Lay L, const float* __restrict__ dHYP, const float* __restrict__ S0,
-                     float* __restrict__ slab, int64_t len, int nsplit, int tiles_j) {
+                     float* __restrict__ slab, int64_t len, int nsplit, int tiles_j, int lin) {
   __shared__ float red[4][DWH_T * (DWH_T + 1)];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int NH = d.NH, S = d.S, M = d.M;
   // 1-D grid, slice-minor: consecutive workgroups go to consecutive XCDs, so with nsplit a multiple of 8 every
   // workgroup of m-slice z runs on XCD z % 8 and the slice's dHYP / S0 rows are fetched into one L2 only
-  const int lin = blockIdx.x, z = lin % nsplit, tile = lin / nsplit;
+  const int z = lin % nsplit, tile = lin / nsplit;
   const int j0 = (tile % tiles_j) * DWH_T, s0 = (tile / tiles_j) * DWH_T;
   // m slice of this workgroup, in 2-row MFMA steps; wave wv takes steps wv, wv + 4, ..
   const int steps = (M + 1) >> 1;
@@ -105,13 +106,29 @@ template <int VAR = 0>
 __global__ __launch_bounds__(256) void dwh_kernel(Dims d, Lay L, const float* __restrict__ dHYP,
                                                   const float* __restrict__ S0, float* __restrict__ slab,
                                                   int64_t len, int nsplit, int tiles_j) {
-  dwh_body<VAR, 8>(d, L, dHYP, S0, slab, len, nsplit, tiles_j);
+  dwh_body<VAR, 8>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, blockIdx.x);
+}
+
+// Horizontal fusion: dW_hyper (blocks [0, ndwh)) beside pass 1 of the slab reduction (blocks [ndwh_pad, ..)) in one
+// launch. Neither reads the other's output (pass 1 covers the BPTT's and the mixer's slabs; dW_hyper's own slabs
+// are summed in pass 2, which reads them directly), so the reduction's HBM reads overlap dW_hyper's MFMA chains
+// instead of following them. ndwh_pad is a multiple of 16, so pass 1's block -> XCD mapping is unchanged.
+__global__ __launch_bounds__(256) void dwh_red1_kernel(Dims d, Lay L, const float* __restrict__ dHYP,
+                                                       const float* __restrict__ S0, float* __restrict__ slab,
+                                                       int64_t len, int nsplit, int tiles_j, int ndwh, int ndwh_pad,
+                                                       RedPlan pl) {
+  const int b = blockIdx.x;
+  if (b < ndwh_pad) {
+    if (b < ndwh) dwh_body<0, 8>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, b);
+    return;
+  }
+  red_pass1_body(pl, b - ndwh_pad);
 }
 
 __global__ __launch_bounds__(256, 10) void dwh_side_kernel(
     Dims d, Lay L, const float* __restrict__ dHYP, const float* __restrict__ S0, float* __restrict__ slab, int64_t len,
     int nsplit, int tiles_j) {
-  dwh_body<0, 2>(d, L, dHYP, S0, slab, len, nsplit, tiles_j);
+  dwh_body<0, 2>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, blockIdx.x);
 }
 
 }  // namespace mq

@@ -97,6 +97,8 @@ struct mq_handle {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // A/B switch: dW_hyper launched between the mixer and the BPTT instead of after the BPTT (same stream)
   bool dwh_first = getenv("MQ_DWH_FIRST") && atoi(getenv("MQ_DWH_FIRST")) != 0;
+  // A/B switch: dW_hyper as its own launch before the reduction (default: fused with reduction pass 1)
+  bool dwh_unfused = getenv("MQ_DWH_UNFUSED") && atoi(getenv("MQ_DWH_UNFUSED")) != 0;
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
   int slots = 0;
   uint32_t mask = 0;
@@ -231,10 +233,17 @@ struct RedBuilder {
   int b1 = 0, b2 = 0;
   float* tmp;
   explicit RedBuilder(float* t) : tmp(t) {}
-  void add(const float* src, int nslab, int64_t len, float* dst, bool sq, int64_t pitch = 0) {
+  void add(const float* src, int nslab, int64_t len, float* dst, bool sq, int64_t pitch = 0, bool direct_ok = false) {
     if (len <= 0 || nslab <= 0) return;
     RedRegion& R = pl.r[pl.nr++];
     R.src = src; R.dst = dst; R.len = len; R.pitch = pitch > 0 ? pitch : len; R.nslab = nslab; R.sq = sq ? 1 : 0;
+    if (direct_ok && nslab <= kRedZ) {   // pass 2 sums the slabs themselves: no pass-1 blocks, no tmp
+      R.zc = 1; R.ng = nslab; R.tmp = (float*)src; R.tpitch = R.pitch; R.vec = 0; R.xcd = 0;
+      R.blk1 = b1;
+      R.blk2 = b2; b2 += (int)((len + 255) / 256);
+      return;
+    }
+    R.tpitch = len;
     // at most kRedZ groups, so pass 2 sums <= 16 partials per element with all loads in flight
     R.zc = (nslab + kRedZ - 1) / kRedZ;
     R.ng = (nslab + R.zc - 1) / R.zc;
@@ -539,7 +548,9 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
       MQ_HIP(launch_gemm(p, mq::H, d.I, ns, s));
     }
   }
-  if (c.mixer == MQ_MIXER_QMIX && !side && !dwh_first) {
+  // dW_hyper runs fused with pass 1 of the reduction (dwh_red1_kernel) unless an A/B switch placed it elsewhere
+  const bool dwh_fused = c.mixer == MQ_MIXER_QMIX && !side && !dwh_first && !h->force_unfused_mix && !h->dwh_unfused;
+  if (c.mixer == MQ_MIXER_QMIX && !side && !dwh_first && !dwh_fused) {
     pt.begin(PH_DWH);
     if (!h->force_unfused_mix) {
       MQ_HIP(launch_dwh(h, d, L, w, s, false));
@@ -557,18 +568,38 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
     pt.end();
     MQ_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
   }
-  pt.begin(PH_RED);
   {
+    int tj = 0, ts = 0, ns = 0, ndwh = 0;
+    if (dwh_fused) {
+      tj = (d.NH + DWH_T - 1) / DWH_T;
+      ts = (d.S + 1 + DWH_T - 1) / DWH_T;
+      ns = std::max(1, std::min({h->dwh_split, kNsplitMax, (d.M + 1) / 2}));
+      h->nsplit_mix = ns;
+      ndwh = tj * ts * ns;
+    }
     RedBuilder rb(w.red_tmp);
     rb.add(w.slab_fc1, h->nsplit_fc1, (int64_t)mq::H * d.I + mq::H, h->grad + h->off[MQ_P_FC1_W], true);
     rb.add(w.slab_rnn, h->nblk_bwd, h->len_rnn, h->grad + h->off[MQ_P_RNN_W_IH], true);
     if (c.mixer == MQ_MIXER_QMIX) {
-      rb.add(w.slab_mix, h->nsplit_mix, h->len_mix, h->grad + h->off[MQ_P_HW1_W], true);
+      // dW_hyper's few m-slice slabs go straight to pass 2 (they are written in the same launch as pass 1)
+      rb.add(w.slab_mix, h->nsplit_mix, h->len_mix, h->grad + h->off[MQ_P_HW1_W], true, 0, true);
       rb.add(w.slab_v2, h->nblk_mix, d.E + 1, h->grad + h->off[MQ_P_V2_W], true);
     }
     rb.add(w.loss_part, h->nblk_mix, MQ_NSUMS, h->grad + h->P, false);
-    hipLaunchKernelGGL(red_pass1_kernel, dim3(rb.b1), dim3(256), 0, s, rb.pl);
-    MQ_HIP(hipGetLastError());
+    if (dwh_fused) {
+      pt.begin(PH_DWH);
+      const int ndwh_pad = (ndwh + 15) / 16 * 16;
+      hipLaunchKernelGGL(dwh_red1_kernel, dim3(ndwh_pad + rb.b1), dim3(256), 0, s, d, L, (const float*)w.dHYP,
+                         (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj, ndwh, ndwh_pad, rb.pl);
+      MQ_HIP(hipGetLastError());
+      pt.begin(PH_RED);
+    } else {
+      pt.begin(PH_RED);
+      if (rb.b1 > 0) {
+        hipLaunchKernelGGL(red_pass1_kernel, dim3(rb.b1), dim3(256), 0, s, rb.pl);
+        MQ_HIP(hipGetLastError());
+      }
+    }
     hipLaunchKernelGGL(red_pass2_kernel, dim3(rb.b2), dim3(256), 0, s, rb.pl, w.norm_part);
     MQ_HIP(hipGetLastError());
     h->n_norm_part = rb.b2;

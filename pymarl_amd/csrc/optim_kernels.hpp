@@ -12,7 +12,8 @@ namespace mq {
 //           (zc chosen so there are at most 16 groups)
 //   pass 2: block (region, chunk) sums the groups in order -> dst, and writes its partial sum of squares of the
 //           gradient elements (regions with sq = 1) for clip_grad_norm_ -> norm_part[block]
-// Fixed summation order throughout: bitwise reproducible.
+// Fixed summation order throughout: bitwise reproducible. A region of at most 16 slabs is "direct": it has no
+// pass-1 blocks and pass 2 sums its slabs in slab order (what pass 1 would have copied, group by group).
 constexpr int kRedZ = 16;
 constexpr int kRedMaxRegions = 6;
 struct RedRegion {
@@ -21,6 +22,7 @@ struct RedRegion {
   float* tmp;
   int64_t len;
   int64_t pitch;    // slab stride in src (>= len: a region may cover a prefix of each slab)
+  int64_t tpitch;   // group stride in tmp (len; pitch for a direct region, whose pass 2 reads the slabs themselves)
   int nslab, zc, ng, sq;
   int vec;          // pass 1 in float4 (len, pitch multiples of 4; src and tmp 16-byte aligned)
   int xcd;          // pass 1 groups slabs by XCD (ng = 16, nslab % 128 == 0, blk1 % 16 == 0): group g holds slabs
@@ -41,11 +43,11 @@ MQ_DEV int red_region(const RedPlan& pl, int b, bool pass2) {
   return k;
 }
 
-__global__ __launch_bounds__(256) void red_pass1_kernel(RedPlan pl) {
-  const int k = red_region(pl, blockIdx.x, false);
+MQ_DEV void red_pass1_body(const RedPlan& pl, int blk) {
+  const int k = red_region(pl, blk, false);
   const RedRegion& R = pl.r[k];
   if (R.vec) {   // 1024 elements per block, one float4 per thread and slab
-    const int nb = (int)((R.len + 1023) / 1024), lb = blockIdx.x - R.blk1;
+    const int nb = (int)((R.len + 1023) / 1024), lb = blk - R.blk1;
     const int g = R.xcd ? lb % R.ng : lb / nb, chunk = R.xcd ? lb / R.ng : lb - g * nb;
     const int64_t i = (int64_t)chunk * 1024 + 4 * threadIdx.x;
     if (i >= R.len) return;
@@ -65,7 +67,7 @@ __global__ __launch_bounds__(256) void red_pass1_kernel(RedPlan pl) {
     *(f32x4*)(R.tmp + (int64_t)g * R.len + i) = s;
     return;
   }
-  const int nb = (int)((R.len + 255) / 256), lb = blockIdx.x - R.blk1;
+  const int nb = (int)((R.len + 255) / 256), lb = blk - R.blk1;
   const int g = R.xcd ? lb % R.ng : lb / nb, chunk = R.xcd ? lb / R.ng : lb - g * nb;
   const int64_t i = (int64_t)chunk * 256 + threadIdx.x;
   if (i >= R.len) return;
@@ -82,6 +84,8 @@ __global__ __launch_bounds__(256) void red_pass1_kernel(RedPlan pl) {
   R.tmp[(int64_t)g * R.len + i] = s;
 }
 
+__global__ __launch_bounds__(256) void red_pass1_kernel(RedPlan pl) { red_pass1_body(pl, blockIdx.x); }
+
 __global__ __launch_bounds__(256) void red_pass2_kernel(RedPlan pl, float* __restrict__ norm_part) {
   const int k = red_region(pl, blockIdx.x, true);
   const RedRegion& R = pl.r[k];
@@ -90,7 +94,7 @@ __global__ __launch_bounds__(256) void red_pass2_kernel(RedPlan pl, float* __res
   if (i < R.len) {
     float u[kRedZ];
 #pragma unroll
-    for (int g = 0; g < kRedZ; ++g) u[g] = g < R.ng ? R.tmp[(int64_t)g * R.len + i] : 0.0f;
+    for (int g = 0; g < kRedZ; ++g) u[g] = g < R.ng ? R.tmp[(int64_t)g * R.tpitch + i] : 0.0f;
     float v = 0.0f;
 #pragma unroll
     for (int g = 0; g < kRedZ; ++g) v += u[g];

@@ -388,6 +388,26 @@ def test_fast_mix_kernel_bitwise(cases, name, monkeypatch):
     assert np.array_equal(outs[0][2], outs[1][2])
 
 
+@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_qmix_ragged", "tiny_qmix", "cfg3_qmix"])
+def test_dwh_fused_reduction_bitwise(cases, name, monkeypatch):
+    """dW_hyper fused with reduction pass 1 (default) equals dW_hyper as its own launch (MQ_DWH_UNFUSED=1) bitwise."""
+    from tests.gpu_helpers import build, flat_grads, flat_params
+    case = get_case(cases, name)
+    outs = []
+    for unfused in ("1", "0"):
+        monkeypatch.setenv("MQ_DWH_UNFUSED", unfused)
+        args, buf, mac, learner, logger = build(case)
+        np.random.seed(case.sampler_seed)
+        for k in range(2):
+            batch = buf.sample(case.B)
+            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
+        th.cuda.synchronize()
+        outs.append((flat_params(learner), flat_grads(learner), learner.last_stats()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]
+
+
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_qmix_ragged", "tiny_qmix"])
 def test_dwh_side_stream_bitwise(cases, name, monkeypatch):
     """dW_hyper on the side stream beside the fused BPTT (MQ_DWH_OVERLAP=1) equals the in-order launch bit for bit."""
