@@ -418,6 +418,8 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   mq_plan plan{};
   plan.rows = d.R;
   plan.inline_ids = rp.nids > 0 ? 1 : 0;
+  const int rw_bwd = std::min(2, pick_rw(d.R, 256));
+  const bool fused_bwd = rw_bwd == 1 && fused_bwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused_bwd;
   const int rw_fwd = pick_rw(d.R, 512);
   if (rw_fwd == 1 && fused_fwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused) {
     plan.fused_fwd = 1;
@@ -488,8 +490,6 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
                          (const float*)h->tg, L, w, curmax);
     MQ_HIP(hipGetLastError());
   }
-  const int rw_bwd = std::min(2, pick_rw(d.R, 256));
-  const bool fused_bwd = rw_bwd == 1 && fused_bwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused_bwd;
   // dW_hyper needs only the mixer's dHYP: forked onto the side stream it runs in the room the fused BPTT leaves on
   // each CU, joined before the reduction (same arithmetic in the same order: bitwise the in-order result)
   const bool side = fused_bwd && c.mixer == MQ_MIXER_QMIX && !h->force_unfused_mix && h->dwh_overlap;
