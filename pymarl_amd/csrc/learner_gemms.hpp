@@ -107,9 +107,14 @@ struct Fc1Prob {
       }
     }
     if (XIN && c.arow) {
+      float* dst = XIN + (int64_t)c.m * d.I + k;
+      if ((d.I & 3) == 0 && k + 3 < ke) {   // one 16-byte store (I % 4 == 0: rows and k-quads 16-B aligned)
+        *(f32x4*)dst = f32x4{r[0], r[1], r[2], r[3]};
+      } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (k + i < ke) XIN[(int64_t)c.m * d.I + k + i] = r[i];
+        for (int i = 0; i < 4; ++i)
+          if (k + i < ke) dst[i] = r[i];
+      }
     }
   }
   MQ_DEV void load_b(const Ctx& c, int pass, int k0, int ke, float (&r)[4]) const {

@@ -56,13 +56,17 @@ def classify_decisions(learner, o, nb, fw):
     top2 = -np.sort(-q[:, 1:], axis=3)[..., :2]
     margin = top2[..., 0] - top2[..., 1]
     tie = margin <= MARGIN_EPS * np.maximum(1.0, np.abs(top2[..., 0]))
+    # live transitions (q_learner.py:39-44 mask): padded slots (every action masked) are ties by construction but
+    # never reach the loss, so they are counted separately
+    live = np.broadcast_to(fw["mask"] > 0, tie.shape)
     got = learner.last_cur_max_actions().cpu().numpy()
     dq_flip = got != fw["cur_max_actions"]
     on_gpu = learner.last_intermediate(3).cpu().numpy() > 0
     pre = fc1_preacts(o.p, nb["obs"], nb["actions_onehot"])
     relu_tie = np.abs(pre) <= RELU_EPS
     relu_flip = on_gpu != (pre > 0)
-    rec = dict(dq_decisions=int(tie.size), dq_ties=int(tie.sum()), dq_flips=int(dq_flip.sum()),
+    rec = dict(dq_decisions=int(live.sum()), dq_ties=int((tie & live).sum()), dq_masked_slots=int((~live).sum()),
+               dq_flips=int(dq_flip.sum()), dq_flips_live=int((dq_flip & live).sum()),
                dq_flips_outside_ties=int((dq_flip & ~tie).sum()), relu_decisions=int(relu_tie.size),
                relu_ties=int(relu_tie.sum()), relu_flips=int(relu_flip.sum()),
                relu_flips_outside_ties=int((relu_flip & ~relu_tie).sum()),
