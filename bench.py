@@ -412,7 +412,10 @@ def coma_bench(a):
                    "state_dim": S, "episode_limit": T, "batch_per_gpu": B, "global_batch": B * world,
                    "replay_episodes": buf.buffer_size, "parallelism": f"dp{world}"},
         "dist": dist_info(world),
-        "roofline": {"bound": "mfma", "kernel": "critic step chain (l1 + head + wgrad, x T)",
+        "roofline": {"bound": "mfma", "kernel": ("coma_chain_kernel (one cooperative launch, T critic steps)"
+                                                 if learner.critic_path() == "chain"
+                                                 else "critic step chain (l1 + head + wgrad, x T)"),
+                     "critic_path": learner.critic_path(),
                      "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "launch_ms": chain_ms / T,
                      "flops_per_launch": step_flops,

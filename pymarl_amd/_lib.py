@@ -29,7 +29,7 @@ EXPORTS = [
     "mq_last_plan", "mq_qmix_forward",
     # include/mc_coma.h
     "mc_create", "mc_destroy", "mc_param_offsets", "mc_bind", "mc_train_step", "mc_update_targets", "mc_policy",
-    "mc_copy_intermediate", "mc_set_timing", "mc_phase_times", "mc_set_data_parallel", "mc_critic_forward",
+    "mc_copy_intermediate", "mc_set_timing", "mc_phase_times", "mc_last_critic_path", "mc_set_data_parallel", "mc_critic_forward",
     "mc_critic_forward_workspace",
 ]
 
@@ -140,6 +140,7 @@ def load(required=True):
         "mc_copy_intermediate": ([vp, ctypes.c_int, vp, ctypes.POINTER(i64), vp], ctypes.c_int),
         "mc_set_timing": ([vp, i32], ctypes.c_int),
         "mc_phase_times": ([vp, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+        "mc_last_critic_path": ([vp], i32),
         "mc_set_data_parallel": ([vp, MC_ALLREDUCE_FN, vp, i32, vp, i64], ctypes.c_int),
     }
     for name, (args, res) in sig.items():

@@ -2,7 +2,7 @@
 // QMIX learner's error handling, replay plumbing and agent kernels. The agent (RNNAgent) forward / BPTT reuses an
 // internal mq_handle (no mixer) for its workspace; the critic has its own.
 #include "../../include/mc_coma.h"
-#include "coma_kernels.hpp"
+#include "coma_chain.hpp"
 
 struct mc_handle {
   mc_config cfg;
@@ -23,6 +23,12 @@ struct mc_handle {
   float *dL, *dHo, *pi, *ppart, *slab_fc2, *red_tmp, *norm_part;
   int last_T = 0, last_R = 0;
   bool timing = false;
+  // persistent critic chain (coma_chain.hpp): off with MQ_COMA_CHAIN=0, or where cc_ok rejects the shape
+  bool chain_env = true;
+  int num_cu = 0;
+  bool chain_attr = false;
+  int last_path = -1;
+  unsigned long long* chain_trace = nullptr;   // MQ_COMA_CHAIN_TRACE=1: phase timestamps printed after each train
   // data parallel (mc_set_data_parallel)
   mc_allreduce_fn dp_fn = nullptr;
   void* dp_ctx = nullptr;
@@ -153,12 +159,12 @@ int mc_create(const mc_config* cfg, mc_handle** out) {
       Tp * R * CH, Tp * R * CH,    // H1t, H2t
       Tp * R * A,                  // Qt
       T * R, T,                    // tgt, msum
-      (int64_t)l1_slices(h->Kp) * R * CH,   // H1p
+      (int64_t)std::max(l1_slices(h->Kp), cc_nk(h->Kc)) * R * CH,   // H1p (three-launch l1 or chain phase A)
       R * CH, R * CH, R * CH, R * CH,   // H1c H2c dH1c dH2c
       R, R,                        // dqc, actc
       T * R * A,                   // qvals
       nhead * 8, nwg, T * 8,       // cpart, cnorm, crec
-      h->Pc, h->Pc,                // shadow params / square_avg
+      h->Pc, h->Pc,                // shadow params / square_avg (the chain's gradient exchange: Pshadow)
       4,                           // cstate
       RTa * h->Ap, RTa * mq::H, RTa * A,   // dL, dHo, pi
       ((RTa + 3) / 4) * 8,         // ppart
@@ -186,6 +192,12 @@ int mc_create(const mc_config* cfg, mc_handle** out) {
   h->cstate = (int*)(b + offs[k++]);
   h->dL = b + offs[k++]; h->dHo = b + offs[k++]; h->pi = b + offs[k++]; h->ppart = b + offs[k++];
   h->slab_fc2 = b + offs[k++]; h->red_tmp = b + offs[k++]; h->norm_part = b + offs[k++];
+  const char* ev = std::getenv("MQ_COMA_CHAIN");
+  h->chain_env = !(ev && ev[0] == '0');
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&h->num_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    h->num_cu = 0;
   *out = h;
   return MQ_OK;
 }
@@ -193,6 +205,7 @@ int mc_create(const mc_config* cfg, mc_handle** out) {
 int mc_destroy(mc_handle* h) {
   if (!h) return MQ_OK;
   if (h->ws) (void)hipFree(h->ws);
+  if (h->chain_trace) (void)hipFree(h->chain_trace);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
   mq_destroy(h->ah);
@@ -291,8 +304,47 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
     MQ_HIP(hipStreamSynchronize(s));
   }
   if (h->timing) MQ_HIP(hipEventRecord(h->ev[1], s));
+  bool chained = false;
+  if (!dp && h->chain_env && cc_ok(R, A, h->Kc, h->num_cu)) {   // every critic step in one cooperative launch
+    CChain cc;
+    cc.d = cd; cc.rp = rp; cc.P = h->critic; cc.SQ = h->csq; cc.G = h->cgrad;
+    cc.o_w1 = ca.o_w1; cc.o_b1 = ca.o_b1; cc.o_w2 = ca.o_w2; cc.o_b2 = ca.o_b2; cc.o_w3 = ca.o_w3; cc.o_b3 = ca.o_b3;
+    cc.Pc = h->Pc; cc.X = h->X; cc.tgt = h->tgt; cc.msum = h->msum; cc.H1p = h->H1p;
+    cc.H1x = h->H1c; cc.H2x = h->H2c; cc.dH2x = h->dH2c; cc.dH1x = h->dH1c; cc.dqx = h->dqc; cc.actx = h->actc;
+    cc.part = h->cpart; cc.normp = h->cnorm; cc.GW = h->Pshadow; cc.qvals = h->qvals;
+    cc.crec = h->crec; cc.cstate = h->cstate; cc.sync = (unsigned*)(h->cstate + 2);   // zeroed above
+    cc.NK = cc_nk(h->Kc); cc.NG = 8 * cc.NK; cc.NHEAD = (R + 15) / 16;
+    cc.hp = ca.hp;
+    const char* tr = std::getenv("MQ_COMA_CHAIN_TRACE");
+    if (tr && tr[0] == '1' && !h->chain_trace) MQ_HIP(hipMalloc(&h->chain_trace, 16 * 8 * sizeof(unsigned long long)));
+    cc.trace = h->chain_trace;
+    const size_t lds = cc_lds_bytes(A);
+    if (!h->chain_attr) {
+      MQ_HIP(hipFuncSetAttribute((const void*)coma_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      h->chain_attr = true;
+    }
+    void* args[] = {&cc};
+    const hipError_t e = hipLaunchCooperativeKernel((const void*)coma_chain_kernel, dim3(cc.NG), dim3(CC_THREADS),
+                                                    args, (unsigned)lds, s);
+    if (e == hipSuccess) {
+      chained = true;
+      if (h->chain_trace) {   // debug: per-phase spans of workgroup 0 (100 MHz clock), averaged over <= 16 steps
+        unsigned long long hb[16 * 8];
+        MQ_HIP(hipMemcpyAsync(hb, h->chain_trace, sizeof(hb), hipMemcpyDeviceToHost, s));
+        MQ_HIP(hipStreamSynchronize(s));
+        double acc[8] = {0};
+        for (int i = 1; i < 15; ++i)
+          for (int k = 0; k < 8; ++k) acc[k] += 10.0 * (double)((k < 7 ? hb[i * 8 + k + 1] : hb[(i + 1) * 8]) - hb[i * 8 + k]);
+        std::fprintf(stderr, "coma_chain ns/step: A %.0f bar1 %.0f B %.0f bar2 %.0f C %.0f bar3 %.0f D %.0f next %.0f\n",
+                     acc[0] / 14, acc[1] / 14, acc[2] / 14, acc[3] / 14, acc[4] / 14, acc[5] / 14, acc[6] / 14, acc[7] / 14);
+      }
+    } else {   // the grid cannot be co-resident here: the three-launch path, from now on
+      (void)hipGetLastError();
+      h->chain_env = false;
+    }
+  }
   int live = 0;
-  for (int t = T - 1; t >= 0; --t) {
+  for (int t = T - 1; t >= 0 && !chained; --t) {
     // live steps before t: exact in data-parallel mode, else assumed none was skipped (the kernels correct it)
     const int Lexp = dp ? live : T - 1 - t;
     hipLaunchKernelGGL(coma_l1_kernel, dim3(ca.KS, CH / 16, (R + kL1Rows - 1) / kL1Rows), dim3(256), lds_l1, s, ca, t,
@@ -308,8 +360,9 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
     }
   }
   MQ_HIP(hipGetLastError());
-  hipLaunchKernelGGL(coma_capply_kernel, dim3((int)std::min<int64_t>((h->Pc + 255) / 256, 512)), dim3(256), 0, s,
-                     ca);
+  if (!chained)
+    hipLaunchKernelGGL(coma_capply_kernel, dim3((int)std::min<int64_t>((h->Pc + 255) / 256, 512)), dim3(256), 0, s,
+                       ca);
   MQ_HIP(hipGetLastError());
   if (dp) {   // per-step critic stat sums; the replicated fields (mask sum, norm, live flag) come from rank 0
     if (h->dp_rank != 0) hipLaunchKernelGGL(coma_dp_crec_kernel, dim3((T + 255) / 256), dim3(256), 0, s, h->crec, T);
@@ -424,6 +477,7 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
                      (const int*)h->cstate, h->stats);
   MQ_HIP(hipGetLastError());
   if (h->timing) MQ_HIP(hipEventRecord(h->ev[3], s));
+  h->last_path = chained ? 1 : 0;
   h->last_T = T;
   h->last_R = R;
   return MQ_OK;
@@ -457,6 +511,8 @@ int mc_phase_times(mc_handle* h, float* ms) {
   for (int i = 0; i < 3; ++i) MQ_HIP(hipEventElapsedTime(&ms[i], h->ev[i], h->ev[i + 1]));
   return MQ_OK;
 }
+
+int32_t mc_last_critic_path(const mc_handle* h) { return h ? h->last_path : -1; }
 
 int mc_update_targets(mc_handle* h, void* stream) {
   if (!h || !h->critic) return set_err(MQ_ERR_STATE, "mc_update_targets before mc_bind");

@@ -847,6 +847,8 @@ __global__ void coma_stats_kernel(const float* __restrict__ crec, int T, const i
   // the agent apply_kernel wrote [loss, norm, sums[2]/msum, sums[3]/msum, sums[4]/msum, msum, coef, 0] at stats + 8
   const float a_loss = stats[8], a_norm = stats[9], a_adv = stats[10], a_pmax = stats[11], a_msum = stats[13];
   for (int k = 0; k < 5; ++k) stats[k] = cnt ? (float)(s[k] / cnt) : 0.0f;
+  if (cstate[3] != 0)   // the persistent critic chain's error word (a grid barrier timed out): loud, not silent
+    for (int k = 0; k < 5; ++k) stats[k] = __builtin_nanf("");
   stats[5] = a_adv;
   stats[6] = a_loss;
   stats[7] = a_norm;

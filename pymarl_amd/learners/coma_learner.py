@@ -252,3 +252,7 @@ class COMALearner:
         ms = (ctypes.c_float * 3)()
         _lib.check(self._handle.lib.mc_phase_times(self._handle.h, ms))
         return {"prologue": ms[0], "critic_chain": ms[1], "actor": ms[2]}
+
+    def critic_path(self):
+        """"chain" (one persistent cooperative launch for the T critic steps), "three_launch", or None before train()."""
+        return {1: "chain", 0: "three_launch"}.get(int(self._handle.lib.mc_last_critic_path(self._handle.h)))

@@ -143,3 +143,43 @@ def test_mac_pi_logits_policy(coma_cases):
             exp = 0.7 * sm + 0.3 / nact
         exp[av == 0] = 0.0
         assert np.abs(got - exp).max() < 1e-5, t
+
+
+@pytest.mark.parametrize("name", ["coma_tiny_masked", "coma_cfg5"])
+def test_coma_chain_matches_three_launch(coma_cases, name, monkeypatch):
+    """The persistent critic chain (coma_chain.hpp, default) against the three-launch path (MQ_COMA_CHAIN=0) from
+    the same state on the same batches: same products, other fixed summation orders for the bias gradients and
+    the norm, so agreement to float rounding amplified along the T-step chain (tolerances as the oracle's)."""
+    from oracle.coma_np import OracleCOMALearner
+    from tests.gpu_helpers import build_coma
+    c = get(coma_cases, name)
+    o = OracleCOMALearner(c.agent_params, c.critic_params, c.cfg())
+    runs = {}
+    for path, env in (("chain", None), ("three_launch", "0")):
+        if env is None:
+            monkeypatch.delenv("MQ_COMA_CHAIN", raising=False)
+        else:
+            monkeypatch.setenv("MQ_COMA_CHAIN", env)
+        args, buf, mac, learner, logger = build_coma(c)
+        np.random.seed(c.sampler_seed)
+        out = []
+        for k in range(2):
+            batch = buf.sample(c.B)
+            batch = batch[:, :batch.max_t_filled()]
+            load_state(learner, o)
+            mac.action_selector.epsilon = c.epsilon[k]
+            learner.train(batch, 1000 * (k + 1), 8 * k)
+            assert learner.critic_path() == path, (name, path)
+            out.append((learner.last_stats(), learner._critic.cpu().numpy().copy(), learner._csq.cpu().numpy().copy(),
+                        learner.last_intermediate(0).cpu().numpy(), learner._agent.cpu().numpy().copy()))
+        runs[path] = out
+    long_chain = c.T > 50
+    for k in range(2):
+        (sa, ca, qa, va, aa), (sb, cb, qb, vb, ab) = runs["chain"][k], runs["three_launch"][k]
+        assert np.abs(ca - cb).max() <= (1e-3 if long_chain else 1e-5), (name, k)
+        assert rel(va, vb) < (1e-3 if long_chain else 1e-5), (name, k)
+        assert rel(qa, qb) < (1e-2 if long_chain else 1e-4), (name, k)
+        assert sa["critic_steps"] == sb["critic_steps"]
+        for s in COMA_STATS:
+            assert np.isfinite(sa[s]), (name, k, s)
+            assert abs(sa[s] - sb[s]) <= (2e-3 if long_chain else 1e-4) * abs(sb[s]) + 1e-5, (name, k, s, sa[s], sb[s])
