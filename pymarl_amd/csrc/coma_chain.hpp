@@ -377,15 +377,24 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
         }
       }
       __syncthreads();
-      if (w < A16 / 16) {   // Q = H2 W3^T + b3
+      {   // Q = H2 W3^T + b3 on all 8 waves: (action tile qn, K part kq); the K parts' partials meet in dH2s (free
+          // until dH2 below) and are summed in kq order
+        const int nat = A16 / 16, ksp = 8 / nat, kw = CH / ksp;   // nat in {1, 2}: 8 or 4 K parts of 16 or 32
+        const int qn = w % nat, kq = w / nat;
         f32x4 acc = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
-#pragma unroll 4
-        for (int k = 0; k < CH; k += 8) {
-          acc = mfma_f32_16x4(H2s[c * CC_CP + k + g], W3s[(16 * w + c) * CC_CP + k + g], acc);
-          acc1 = mfma_f32_16x4(H2s[c * CC_CP + k + 4 + g], W3s[(16 * w + c) * CC_CP + k + 4 + g], acc1);
+        for (int k = kq * kw; k < (kq + 1) * kw; k += 8) {
+          acc = mfma_f32_16x4(H2s[c * CC_CP + k + g], W3s[(16 * qn + c) * CC_CP + k + g], acc);
+          acc1 = mfma_f32_16x4(H2s[c * CC_CP + k + 4 + g], W3s[(16 * qn + c) * CC_CP + k + 4 + g], acc1);
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Qs[(4 * g + e) * (A16 + 1) + 16 * w + c] = (acc[e] + acc1[e]) + b3s[16 * w + c];
+        for (int e = 0; e < 4; ++e) dH2s[(kq * 16 + 4 * g + e) * A16 + 16 * qn + c] = acc[e] + acc1[e];
+        __syncthreads();
+        if (tid < 16 * A16) {
+          const int i = tid / A16, j = tid - i * A16;
+          float q = 0.0f;
+          for (int p = 0; p < ksp; ++p) q += dH2s[(p * 16 + i) * A16 + j];
+          Qs[i * (A16 + 1) + j] = q + b3s[j];
+        }
       }
       __syncthreads();
       float* dqs = misc;              // [16]
@@ -498,17 +507,19 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
       __syncthreads();
       // waves 0 .. 6: the dW1 tile's 7 N-tiles; wave 5 then db1 (ks = 0), wave 6 then its dW3 tiles; wave 7: dW2
       if (w < 7) {   // dW1 tile, N-tile w: A[i = unit][kk = row] = dH1, B[kk = row][j = column] = X_t
-        f32x4 acc = {0, 0, 0, 0};
-        for (int rr = 0; rr < R; rr += 4) {
-          const int row = rr + g;
+        f32x4 acc = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};   // two interleaved k-chains (even / odd 4-row steps)
+#pragma unroll
+        for (int q = 0; q < CC_MAXR / 4; ++q) {
+          const int row = 4 * q + g;
           const float av = row < R ? Du[row * 17 + c] : 0.0f;
           const float bv = row < R ? Xs[row * CC_KP + 16 * w + c] : 0.0f;
-          acc = mfma_f32_16x4(av, bv, acc);
+          if (q & 1) acc1 = mfma_f32_16x4(av, bv, acc1);
+          else acc = mfma_f32_16x4(av, bv, acc);
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const bool valid = 16 * w + c < kwc;
-          gl1[e] = valid ? acc[e] : 0.0f;   // raw (unnormalised) gradient until phase D
+          gl1[e] = valid ? acc[e] + acc1[e] : 0.0f;   // raw (unnormalised) gradient until phase D
           sq = fmaf(gl1[e], gl1[e], sq);
         }
       }
@@ -523,14 +534,19 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
         for (int qt = wg; qt < 64; qt += a.NG) {
           const int qu = qt >> 3, qj = qt & 7;
           if (qt != wg) load_w2(qt);
-          f32x4 acc = {0, 0, 0, 0};
+          f32x4 acc = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
           float bs = 0.0f;
 #pragma unroll
-          for (int q = 0; q < CC_MAXR / 4; ++q) { acc = mfma_f32_16x4(pA[q], pB[q], acc); bs += pA[q]; }
+          for (int q = 0; q < CC_MAXR / 4; ++q) {
+            if (q & 1) acc1 = mfma_f32_16x4(pA[q], pB[q], acc1);
+            else acc = mfma_f32_16x4(pA[q], pB[q], acc);
+            bs += pA[q];
+          }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            st_wt(&a.GW[a.o_w2 + (int64_t)(16 * qu + 4 * g + e) * CH + 16 * qj + c], acc[e]);
-            sq = fmaf(acc[e], acc[e], sq);
+            const float gv = acc[e] + acc1[e];
+            st_wt(&a.GW[a.o_w2 + (int64_t)(16 * qu + 4 * g + e) * CH + 16 * qj + c], gv);
+            sq = fmaf(gv, gv, sq);
           }
           if (qj == 0) {   // db2 of the tile's units: lane groups g hold rows g, g + 4, ..: combine the four
             bs += __shfl_xor(bs, 16, 64);
@@ -549,18 +565,21 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
           if (qt != wg) load_w3(qt);
           f32x4 acc = {0, 0, 0, 0};
           float bs = 0.0f;
+          f32x4 acc1 = {0, 0, 0, 0};
 #pragma unroll
           for (int q = 0; q < CC_MAXR / 4; ++q) {
             const float av = pI[q] == aa ? pA[q] : 0.0f;
-            acc = mfma_f32_16x4(av, pB[q], acc);
+            if (q & 1) acc1 = mfma_f32_16x4(av, pB[q], acc1);
+            else acc = mfma_f32_16x4(av, pB[q], acc);
             bs += av;
           }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int arow = 16 * qa + 4 * g + e;
             if (arow < A) {
-              st_wt(&a.GW[a.o_w3 + (int64_t)arow * CH + 16 * qj + c], acc[e]);
-              sq = fmaf(acc[e], acc[e], sq);
+              const float gv = acc[e] + acc1[e];
+              st_wt(&a.GW[a.o_w3 + (int64_t)arow * CH + 16 * qj + c], gv);
+              sq = fmaf(gv, gv, sq);
             }
           }
           if (qj == 0) {   // db3

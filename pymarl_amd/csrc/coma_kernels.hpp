@@ -830,20 +830,40 @@ __global__ __launch_bounds__(256) void coma_dp_crec_kernel(float* __restrict__ c
 // reference logs them (reversed t), then the actor's stats from the agent apply (stats[8..11] scratch on entry).
 __global__ void coma_stats_kernel(const float* __restrict__ crec, int T, const int* __restrict__ cstate,
                                   float* __restrict__ stats) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  // one wave: lane l takes steps l, l + 64, .. (all loads in flight), then a fixed butterfly over the lanes
+  // (a single thread walking T records was ~61 us at T = 180: one dependent load chain)
+  if (blockIdx.x != 0) return;
+  const int lane = threadIdx.x;
   double s[5] = {0, 0, 0, 0, 0};
-  int cnt = 0;
-  for (int t = T - 1; t >= 0; --t) {
-    const float* rec = crec + t * 8;
-    if (rec[6] == 0.0f) continue;
-    const double msum = rec[1];
-    s[0] += (double)(rec[0] / rec[1]);
-    s[1] += (double)rec[5];
-    s[2] += (double)rec[2] / msum;
-    s[3] += (double)rec[3] / msum;
-    s[4] += (double)rec[4] / msum;
-    ++cnt;
+  double cntd = 0.0;
+  for (int t0 = 0; t0 < T; t0 += 256) {
+    float r[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = t0 + lane + 64 * j;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[j][k] = t < T ? crec[t * 8 + k] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (r[j][6] == 0.0f) continue;
+      const double msum = r[j][1];
+      s[0] += (double)(r[j][0] / r[j][1]);
+      s[1] += (double)r[j][5];
+      s[2] += (double)r[j][2] / msum;
+      s[3] += (double)r[j][3] / msum;
+      s[4] += (double)r[j][4] / msum;
+      cntd += 1.0;
+    }
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) s[k] += __shfl_xor(s[k], o, 64);
+    cntd += __shfl_xor(cntd, o, 64);
+  }
+  if (lane != 0) return;
+  const int cnt = (int)cntd;
   // the agent apply_kernel wrote [loss, norm, sums[2]/msum, sums[3]/msum, sums[4]/msum, msum, coef, 0] at stats + 8
   const float a_loss = stats[8], a_norm = stats[9], a_adv = stats[10], a_pmax = stats[11], a_msum = stats[13];
   for (int k = 0; k < 5; ++k) stats[k] = cnt ? (float)(s[k] / cnt) : 0.0f;
