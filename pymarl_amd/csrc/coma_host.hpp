@@ -165,7 +165,7 @@ int mc_create(const mc_config* cfg, mc_handle** out) {
       T * R * A,                   // qvals
       nhead * 8, nwg, T * 8,       // cpart, cnorm, crec
       h->Pc, h->Pc,                // shadow params / square_avg (the chain's gradient exchange: Pshadow)
-      4,                           // cstate
+      8,                           // cstate (+ the critic chain's sync words)
       RTa * h->Ap, RTa * mq::H, RTa * A,   // dL, dHo, pi
       ((RTa + 3) / 4) * 8,         // ppart
       ns2 * (A * mq::H + A),       // slab_fc2
@@ -253,7 +253,7 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
 
   if (h->timing) MQ_HIP(hipEventRecord(h->ev[0], s));
   MQ_HIP(hipMemsetAsync(h->crec, 0, (size_t)T * 8 * sizeof(float), s));
-  MQ_HIP(hipMemsetAsync(h->cstate, 0, 4 * sizeof(int), s));
+  MQ_HIP(hipMemsetAsync(h->cstate, 0, 8 * sizeof(int), s));
   hipLaunchKernelGGL(coma_mask_kernel, dim3((T + 255) / 256), dim3(256), 0, s, cd, rp, h->msum);
   MQ_HIP(hipGetLastError());
   const bool dp = h->dp_fn != nullptr;
