@@ -183,3 +183,42 @@ def test_coma_chain_matches_three_launch(coma_cases, name, monkeypatch):
         for s in COMA_STATS:
             assert np.isfinite(sa[s]), (name, k, s)
             assert abs(sa[s] - sb[s]) <= (2e-3 if long_chain else 1e-4) * abs(sb[s]) + 1e-5, (name, k, s, sa[s], sb[s])
+
+
+@pytest.mark.parametrize("path,env", [("chain", None), ("three_launch", "0")])
+def test_coma_skipped_critic_steps(path, env, monkeypatch):
+    """Steps whose mask is empty for every episode are skipped (coma_learner.py:121-122): slot 2 and slot 5 are
+    made unwritten (filled = 0, no action) in every episode of the masked tiny case. Teacher-forced against the
+    oracle through both critic paths; critic_steps counts the live steps only."""
+    from oracle.coma_np import OracleCOMALearner
+    from tests.gpu_helpers import build_coma
+    if env is None:
+        monkeypatch.delenv("MQ_COMA_CHAIN", raising=False)
+    else:
+        monkeypatch.setenv("MQ_COMA_CHAIN", env)
+    c = ComaCase("coma_tiny_masked")
+    for h in (2, 5):
+        c.data["filled"][:, h] = 0
+        c.data["actions"][:, h] = 0
+        c.data["actions_onehot"][:, h] = 0.0
+    args, buf, mac, learner, logger = build_coma(c)
+    o = OracleCOMALearner(c.agent_params, c.critic_params, c.cfg())
+    np.random.seed(c.sampler_seed)
+    batch = buf.sample(c.B)
+    batch = batch[:, :batch.max_t_filled()]
+    nb, _ = c.batch(0)
+    load_state(learner, o)
+    mac.action_selector.epsilon = c.epsilon[0]
+    learner.train(batch, 1000, 0)
+    assert learner.critic_path() == path
+    st = learner.last_stats()
+    so = o.train(nb, 1000, 0, c.epsilon[0])
+    live = len(o.last["critic_grads"])
+    T = nb["filled"].shape[1] - 1
+    assert live <= T - 2, (live, T)   # the two holes were skipped
+    assert int(round(st["critic_steps"])) == live
+    assert rel(learner.last_intermediate(0).cpu().numpy(), o.last["q_vals"]) < 1e-5
+    for s in COMA_STATS:
+        assert abs(st[s] - so[s]) <= 1e-4 * abs(so[s]) + 1e-6, (path, s, st[s], so[s])
+    dc = np.abs(learner._critic.cpu().numpy() - o.flat("critic")).max()
+    assert dc <= 5e-4 * 20, dc
