@@ -6,7 +6,7 @@
 // gradient in registers, so W1 (the critic's 111k-element bulk at MMM2) never leaves the CU between steps. The first
 // NHEAD = ceil(R / 16) workgroups also run the head of one 16-row tile. fc1.bias / fc2 / fc3 live in P (the caller's
 // buffer): every workgroup applies the update to a 1/G slice of them in place, and the heads reload the new version
-// into LDS at the start of the next step. One live step t is four phases with a grid barrier after the first three:
+// into LDS at the start of the next step. One live step t is four phases:
 //   A  (all)   H1p[ks][r][16 ut ..] = X_t[r][K slice] W1_tile^T                         (MFMA; X_t prefetched)
 //   B  (heads) reload b1 / W2 / b2 / W3 / b3, H1 = relu(sum_ks H1p + b1), H2 = relu(H1 W2^T + b2), Q = H2 W3^T + b3,
 //              TD error vs the TD(lambda) target, loss sums, dQ, dH2 = dQ W3 o [H2 > 0], dH1 = dH2 W2 o [H1 > 0]
@@ -14,10 +14,14 @@
 //              the dW3 tiles round-robin over the workgroups, per-workgroup sum of squares
 //   D  (all)   the global gradient norm from the G partials (fixed order), clip coefficient, RMSprop on the owned
 //              W1 tile and on the owned slice of fc1.bias .. fc3.bias; workgroup 0 records the stats
+// The hand-offs are flags, not grid barriers: A -> B every workgroup flags, only the heads wait; B -> C the heads
+// flag, every workgroup waits; C -> D each workgroup publishes its sum of squares as one 8-B {value, step tag}
+// granule after draining its stores, and every workgroup's wave 0 polls all G granules. Buffers reused by the next
+// step are safe because each write of step t + 1 sits behind a wait on flags posted after the step-t reads.
 // Hand-offs between workgroups: every exchanged word is stored write-through (sc1) and loaded sc1 by the consumer
-// (4-B, or 16-B where the layout allows), after a counter barrier (every wave drains its stores, workgroup barrier,
-// one agent-scope atomic add, one lane polls the counter sc1 with s_sleep) — MI355X_MICROARCH.md § visibility, Valid
-// forms, row 1; no cache fences. Spins are bounded: a timeout sets the error word, every workgroup leaves, and the
+// (4-B, or 16-B where the layout allows), behind step-tagged flags (every wave drains its stores, workgroup barrier,
+// one lane stores the flag write-through; the consumer polls sc1 with s_sleep) — MI355X_MICROARCH.md § visibility,
+// Valid forms, row 1; no cache fences. Spins are bounded: a timeout sets the error word, every workgroup leaves, and the
 // stats come out NaN. Skipped steps (empty mask, coma_learner.py:121-122) are skipped by every workgroup alike.
 // The products are the three-launch path's; the bias gradients (db1 in row order, db2 / db3 as per-lane partials
 // combined over the four lane groups), the norm partials and the H2 / Q / dH1 k-chains (two interleaved
@@ -41,6 +45,7 @@ constexpr int CC_XV = CC_KW / 4;                                     // 16-B uni
 constexpr int CC_XPT = (CC_MAXR * CC_XV + CC_THREADS - 1) / CC_THREADS;  // of them per thread
 
 typedef __attribute__((address_space(1))) unsigned cc_gu32;
+typedef __attribute__((address_space(1))) unsigned long long cc_gu64;
 
 MQ_DEV void st_wt(float* p, float v) {
   __hip_atomic_store((cc_gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -86,12 +91,14 @@ struct CChain {
   float* dqx;         // [R]
   int* actx;          // [R]
   float* part;        // [NHEAD][8]
-  float* normp;       // [G]
+  unsigned long long* normg;   // [G] {sum of squares, step tag} granules (zeroed before the launch)
   float* GW;          // [Pc] gradient exchange (b1, W2, b2, W3, b3 regions)
   float* qvals;       // [T][R][A]
   float* crec;        // [T][8]
   int* cstate;        // [0] live steps, [1] t of the last live step
-  unsigned* sync;     // [0] barrier counter, [1] error word (zeroed before the launch)
+  unsigned* sync;     // [1] error word (zeroed before the launch)
+  unsigned* flagA;    // [G] phase-A-done step tags (zeroed before the launch)
+  unsigned* flagB;    // [NHEAD] phase-B-done step tags of the heads
   int NK, NG, NHEAD;
   OptHP hp;
   unsigned long long* trace;   // optional (MQ_COMA_CHAIN_TRACE): workgroup 0's phase timestamps, [16 steps][8]
@@ -137,26 +144,36 @@ inline bool cc_ok(int R, int A, int Kc, int num_cu) {
          8 * cc_nk(Kc) >= (R + 15) / 16 && 8 * cc_nk(Kc) <= 256;
 }
 
-// Grid barrier number `k` (1-based): every wave drains its write-through stores, one lane adds to the counter and
-// polls it until all G workgroups have added k times. Returns false (error word set) on a timeout or a peer's error.
-MQ_DEV bool cc_barrier(const CChain& a, unsigned k, float* misc) {
+// Hand-off flags (MI355X_MICROARCH.md Valid forms row 1): the publisher drains every wave's write-through stores,
+// joins a workgroup barrier, and one lane stores the step tag to its flag word write-through; a consumer's wave 0
+// polls the `count` flags it depends on (lane i: flags i, i + 64, ..) until each reaches the tag, and the other
+// waves join behind a workgroup barrier. Tags grow by one per live step and the words are zeroed per launch.
+// Returns false (error word set) on a timeout or a peer's error.
+MQ_DEV void cc_post(unsigned* flag, unsigned tag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add((cc_gu32*)a.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned target = k * (unsigned)a.NG;
-    unsigned spins = 0;
-    int ok = 1;
-    while (__hip_atomic_load((cc_gu32*)a.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (++spins > CC_SPIN_LIMIT ||
-          __hip_atomic_load((cc_gu32*)(a.sync + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-        ok = 0;
-        break;
+  if (threadIdx.x == 0) __hip_atomic_store((cc_gu32*)flag, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+MQ_DEV bool cc_wait(const CChain& a, const unsigned* flags, int count, unsigned tag, float* misc) {
+  if (threadIdx.x < 64) {
+    int fail = 0;
+    for (int i = threadIdx.x; i < count && !fail; i += 64) {
+      unsigned spins = 0;
+      while (__hip_atomic_load((cc_gu32*)(unsigned*)(flags + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < tag) {
+        if (++spins > CC_SPIN_LIMIT ||
+            __hip_atomic_load((cc_gu32*)(a.sync + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+          fail = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
       }
-      __builtin_amdgcn_s_sleep(2);
     }
-    if (!ok) __hip_atomic_store((cc_gu32*)(a.sync + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    misc[63] = ok ? 1.0f : 0.0f;
+    const bool any = __ballot(fail) != 0ull;
+    if (threadIdx.x == 0) {
+      if (any) __hip_atomic_store((cc_gu32*)(a.sync + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      misc[63] = any ? 0.0f : 1.0f;
+    }
   }
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the exchanged-data loads below the poll
@@ -239,7 +256,6 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
     return -1;
   };
   load_x(next_live(T), tid);
-  unsigned bk = 0;
   int live = 0, last_t = -1;
   int td_at = 0;
   float td_m = 0.0f, td_y = 0.0f;
@@ -297,7 +313,9 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
       }
     }
     stamp(1);
-    if (!(ok = cc_barrier(a, ++bk, misc))) break;
+    // A -> B: every workgroup flags its H1 partials (and the phase-D stores before them); only the heads wait
+    cc_post(a.flagA + wg, (unsigned)(live + 1));
+    if (head && !(ok = cc_wait(a, a.flagA, a.NG, (unsigned)(live + 1), misc))) break;
     stamp(2);
     load_x(next_live(t), tid);   // lands while the heads run phase B
     // ================================================================ B: the head of rows r0 .. r0 + 15
@@ -457,7 +475,9 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
       }
     }
     stamp(3);
-    if (!(ok = cc_barrier(a, ++bk, misc))) break;
+    // B -> C: the heads flag H1 / H2 / dH2 / dH1 / dQ / actions / loss partials; every workgroup waits for them
+    if (head) cc_post(a.flagB + wg, (unsigned)(live + 1));
+    if (!(ok = cc_wait(a, a.flagB, a.NHEAD, (unsigned)(live + 1), misc))) break;
     stamp(4);
     // ================================================================ C: gradients, per-workgroup sum of squares
     float sq = 0.0f;
@@ -594,23 +614,49 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
       }
       sq = wave_sum(sq);
       if (lane == 0) misc[32 + w] = sq;   // misc[32 .. 39]: per-wave partials
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's write-through stores of C drained ...
       __syncthreads();
-      if (tid == 0) {
+      if (tid == 0) {   // ... before this workgroup's {sum of squares, step tag} granule: its flag for phase D
         float s = 0.0f;
         for (int i = 0; i < CC_THREADS / 64; ++i) s += misc[32 + i];
-        st_wt(&a.normp[wg], s);
+        const unsigned long long gv = ((unsigned long long)(unsigned)(live + 1) << 32) | __float_as_uint(s);
+        __hip_atomic_store((cc_gu64*)(a.normg + wg), gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     stamp(5);
-    if (!(ok = cc_barrier(a, ++bk, misc))) break;
+    // no counter barrier here: wave 0 polls the G granules (one 8-B write-through store each, MI355X_MICROARCH.md
+    // Valid forms: R2 granules / row 1 flags), and the other waves join behind the workgroup barrier below
     stamp(6);
     // ================================================================ D: clip + RMSprop (coma_learner.py:132-134)
     float* np_s = H1s;   // head scratch is dead in phase D: workgroup 0's copy of the loss partials
     if (w == 0) {   // the squared norm: each lane sums its partials (lane, lane + 64, ..), then a fixed butterfly
       float pv[4];
+      const unsigned tag = (unsigned)(live + 1);
+      int fail = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pv[j] = lane + 64 * j < a.NG ? ld_wt(&a.normp[lane + 64 * j]) : 0.0f;
+      for (int j = 0; j < 4; ++j) {
+        pv[j] = 0.0f;
+        const int i = lane + 64 * j;
+        if (i < a.NG) {
+          unsigned spins = 0;
+          unsigned long long gv;
+          while (((gv = __hip_atomic_load((cc_gu64*)(a.normg + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) !=
+                 tag) {
+            if (++spins > CC_SPIN_LIMIT ||
+                __hip_atomic_load((cc_gu32*)(a.sync + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+              fail = 1;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+          pv[j] = __uint_as_float((unsigned)gv);
+        }
+      }
       const float s = wave_sum((pv[0] + pv[1]) + (pv[2] + pv[3]));
+      if (__ballot(fail) != 0ull) {
+        if (lane == 0) __hip_atomic_store((cc_gu32*)(a.sync + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (lane == 0) misc[63] = __ballot(fail) != 0ull ? 0.0f : 1.0f;
       if (lane == 0) {
         const float inv = 1.0f / mt;
         const float norm = sqrtf(s) * inv;
@@ -618,10 +664,12 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
         misc[49] = fminf(a.hp.clip / (norm + 1e-6f), 1.0f);
         misc[50] = norm;
       }
-    } else if (w == 1 && wg == 0) {
+    } else if (w == 1 && wg == 0) {   // written in phase B: ordered by barrier 2
       if (lane < 8 * a.NHEAD) np_s[256 + lane] = ld_wt(&a.part[lane]);
     }
     __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the exchanged-data loads below the poll
+    if (misc[63] == 0.0f) { ok = false; break; }
     const float inv = misc[48], coef = misc[49];
     if (w < 7) {
 #pragma unroll

@@ -163,7 +163,7 @@ int mc_create(const mc_config* cfg, mc_handle** out) {
       R * CH, R * CH, R * CH, R * CH,   // H1c H2c dH1c dH2c
       R, R,                        // dqc, actc
       T * R * A,                   // qvals
-      nhead * 8, nwg, T * 8,       // cpart, cnorm, crec
+      nhead * 8, std::max<int64_t>(nwg, 1024), T * 8,   // cpart, cnorm (chain: 256 8-B granules + flags), crec
       h->Pc, h->Pc,                // shadow params / square_avg (the chain's gradient exchange: Pshadow)
       8,                           // cstate (+ the critic chain's sync words)
       RTa * h->Ap, RTa * mq::H, RTa * A,   // dL, dHo, pi
@@ -311,13 +311,17 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
     cc.o_w1 = ca.o_w1; cc.o_b1 = ca.o_b1; cc.o_w2 = ca.o_w2; cc.o_b2 = ca.o_b2; cc.o_w3 = ca.o_w3; cc.o_b3 = ca.o_b3;
     cc.Pc = h->Pc; cc.X = h->X; cc.tgt = h->tgt; cc.msum = h->msum; cc.H1p = h->H1p;
     cc.H1x = h->H1c; cc.H2x = h->H2c; cc.dH2x = h->dH2c; cc.dH1x = h->dH1c; cc.dqx = h->dqc; cc.actx = h->actc;
-    cc.part = h->cpart; cc.normp = h->cnorm; cc.GW = h->Pshadow; cc.qvals = h->qvals;
+    cc.part = h->cpart; cc.normg = (unsigned long long*)h->cnorm; cc.GW = h->Pshadow; cc.qvals = h->qvals;
     cc.crec = h->crec; cc.cstate = h->cstate; cc.sync = (unsigned*)(h->cstate + 2);   // zeroed above
     cc.NK = cc_nk(h->Kc); cc.NG = 8 * cc.NK; cc.NHEAD = (R + 15) / 16;
     cc.hp = ca.hp;
     const char* tr = std::getenv("MQ_COMA_CHAIN_TRACE");
     if (tr && tr[0] == '1' && !h->chain_trace) MQ_HIP(hipMalloc(&h->chain_trace, 16 * 8 * sizeof(unsigned long long)));
     cc.trace = h->chain_trace;
+    // cnorm: [0, 2 G) the norm granules, [512, 512 + G) flagA, [768, 768 + NHEAD) flagB; no stale step tags
+    cc.flagA = (unsigned*)(h->cnorm + 512);
+    cc.flagB = (unsigned*)(h->cnorm + 768);
+    MQ_HIP(hipMemsetAsync(h->cnorm, 0, 1024 * sizeof(float), s));
     const size_t lds = cc_lds_bytes(A);
     if (!h->chain_attr) {
       MQ_HIP(hipFuncSetAttribute((const void*)coma_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
