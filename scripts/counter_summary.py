@@ -22,7 +22,7 @@ from collections import defaultdict
 
 PHASES = {"Fc1Prob": "fc1", "GiProb": "gi", "gru_fwd": "gru_fwd", "Fc2Prob": "fc2", "HypProb": "hyper",
           "hyper_ws_kernel": "hyper", "hyper_kernel": "hyper", "mix_kernel": "mix", "mix_fast_kernel": "mix",
-          "gru_bwd": "gru_bwd", "Dx1Prob": "dx1", "Dw1Prob": "dw1", "DwhProb": "dwh", "dwh_kernel": "dwh",
+          "gru_bwd": "gru_bwd", "Dx1Prob": "dx1", "Dw1Prob": "dw1", "DwhProb": "dwh", "dwh_kernel": "dwh", "dwh_red1": "dwh",
           "red_pass": "reduce", "apply_kernel": "apply", "coma_l1": "coma_l1", "coma_head": "coma_head",
           "coma_wgrad": "coma_wgrad", "coma_chain": "coma_chain"}
 SIMDS = 1024
