@@ -256,23 +256,6 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     for (int i = 0; i < 7; ++i) acc_w1[i] = f32x4{0, 0, 0, 0};
     f32x4 dxa = {0, 0, 0, 0}, dxb = {0, 0, 0, 0};
     float db1p = 0.0f;
-    // VAR 8192 (timing only, wrong gradients): the producers issue packed-FMA VALU work of the same FLOPs as their
-    // MFMAs (8 v_pk_fma_f32 per lane per 16x16x4 MFMA) with LDS operands, instead of the MFMAs
-    constexpr bool kValu = (VAR & 8192) != 0;
-    typedef float v2f __attribute__((ext_vector_type(2)));
-    v2f vacc[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) vacc[j] = v2f{0.0f, 0.0f};
-    auto valu_work = [&](int C, int nmf) {
-      const int cb = C & 1;
-      const f32x4 o0 = *(const f32x4*)&S.gi[cb][c16][4 * g];
-      const f32x4 o1 = *(const f32x4*)&S.gh[cb][c16][4 * g];
-      const v2f a0 = {o0[0], o0[1]}, a1 = {o0[2], o0[3]}, b0 = {o1[0], o1[1]}, b1 = {o1[2], o1[3]};
-      for (int r = 0; r < nmf; ++r) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) vacc[j] = ((j & 1) ? a1 : a0) * ((j & 2) ? b1 : b0) + vacc[j];
-      }
-    };
 
     // X1 / XIN rows of a chunk: slot s of this thread covers element ptid + 256 s of [16][H] and of [16][I]
     constexpr int NX1 = FCH * H / 256, NXI = (FCH * 4 * FKQ + 255) / 256;
@@ -396,11 +379,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
         if (t >= Tp) continue;
         lds_barrier();   // step t's records published
         fc2_grads(t);
-        if (work && kValu) {
-          if (u == 0 && !(VAR & 512)) issue_rows(C);
-          if (u == 4) store_rows(C);
-          valu_work(C, (u >= 1 && u <= 12) ? 12 : (u == 15 ? 14 : (u >= 13 ? 7 : 0)));
-        } else if (work) {
+        if (work) {
           if (u == 0 && !(VAR & 512)) issue_rows(C);
           if (u >= 1 && u <= 4) dw_rec(C, u - 1, u, false);
           if (u == 4) store_rows(C);
@@ -430,12 +409,6 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     lds_barrier();
     if (!(VAR & 4)) dw1_part(0, 4);
 
-    if (kValu) {   // keep the timing-only VALU work live
-      float sv = 0.0f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sv += vacc[j][0] + vacc[j][1];
-      acc_hh[0][0][0] += sv;
-    }
     // per-workgroup slabs in the MFMA C layout: element (16 tile + 4 g + e, 16 tile' + c16)
 #pragma unroll
     for (int i = 0; i < 3; ++i)

@@ -231,17 +231,6 @@ int main(int argc, char** argv) {
       std::sort(a.begin(), a.end()); std::sort(b.begin(), b.end());
       printf("fused bwd V0 median %.1f min %.1f | V128 median %.1f min %.1f\n", a[4], a[0], b[4], b[0]);
     }
-    {
-      std::vector<float> a, b, c;
-      for (int round = 0; round < 7; ++round) {
-        a.push_back(runbf(gru_bwd_fused_kernel<768>));
-        b.push_back(runbf(gru_bwd_fused_kernel<772>));
-        c.push_back(runbf(gru_bwd_fused_kernel<768 + 8192>));
-      }
-      std::sort(a.begin(), a.end()); std::sort(b.begin(), b.end()); std::sort(c.begin(), c.end());
-      printf("fused bwd medians: V768 %.1f | V772 (producers idle) %.1f | V8960 (VALU producers, timing only) %.1f\n",
-             a[3], b[3], c[3]);
-    }
     printf("fused bwd V768 %.1f us | V772 (producers idle) %.1f | V1792 (SIMD split) %.1f | V1796 %.1f\n",
            runbf(gru_bwd_fused_kernel<768>), runbf(gru_bwd_fused_kernel<772>), runbf(gru_bwd_fused_kernel<1792>),
            runbf(gru_bwd_fused_kernel<1796>));
