@@ -102,6 +102,8 @@ struct CChain {
   int NK, NG, NHEAD;
   OptHP hp;
   unsigned long long* trace;   // optional (MQ_COMA_CHAIN_TRACE): workgroup 0's phase timestamps, [16 steps][8]
+  int fault_wg;                // test hook (MQ_COMA_CHAIN_FAULT): this workgroup never flags its phase A of the
+                               // second live step, so the heads time out (-1: none)
 };
 
 // LDS carve (floats)
@@ -314,7 +316,7 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
     }
     stamp(1);
     // A -> B: every workgroup flags its H1 partials (and the phase-D stores before them); only the heads wait
-    cc_post(a.flagA + wg, (unsigned)(live + 1));
+    if (!(wg == a.fault_wg && live == 1)) cc_post(a.flagA + wg, (unsigned)(live + 1));
     if (head && !(ok = cc_wait(a, a.flagA, a.NG, (unsigned)(live + 1), misc))) break;
     stamp(2);
     load_x(next_live(t), tid);   // lands while the heads run phase B

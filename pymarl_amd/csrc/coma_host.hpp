@@ -318,6 +318,8 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
     const char* tr = std::getenv("MQ_COMA_CHAIN_TRACE");
     if (tr && tr[0] == '1' && !h->chain_trace) MQ_HIP(hipMalloc(&h->chain_trace, 16 * 8 * sizeof(unsigned long long)));
     cc.trace = h->chain_trace;
+    const char* fe = std::getenv("MQ_COMA_CHAIN_FAULT");   // test hook: a workgroup that stops flagging
+    cc.fault_wg = fe ? std::atoi(fe) : -1;
     // cnorm: [0, 2 G) the norm granules, [512, 512 + G) flagA, [768, 768 + NHEAD) flagB; no stale step tags
     cc.flagA = (unsigned*)(h->cnorm + 512);
     cc.flagB = (unsigned*)(h->cnorm + 768);

@@ -873,7 +873,7 @@ __global__ void coma_stats_kernel(const float* __restrict__ crec, int T, const i
   stats[6] = a_loss;
   stats[7] = a_norm;
   stats[8] = a_pmax;
-  stats[9] = (float)cstate[0];
+  stats[9] = cstate[3] != 0 ? -1.0f : (float)cstate[0];   // -1: the critic chain failed (the learner raises)
   stats[10] = a_msum;
 }
 

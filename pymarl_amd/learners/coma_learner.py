@@ -166,6 +166,9 @@ class COMALearner:
         del keep
         st = self._stats.tolist()   # the one synchronisation per train(): stats + critic step count
         steps = int(round(st[9]))
+        if steps < 0:
+            raise _lib.MQError("COMA critic chain: a workgroup hand-off timed out; this train()'s critic update is "
+                               "invalid (MQ_COMA_CHAIN=0 selects the three-launch critic)")
         self.critic_training_steps += steps
         self._steps += 1
         for p in self.agent_params:

@@ -222,3 +222,27 @@ def test_coma_skipped_critic_steps(path, env, monkeypatch):
         assert abs(st[s] - so[s]) <= 1e-4 * abs(so[s]) + 1e-6, (path, s, st[s], so[s])
     dc = np.abs(learner._critic.cpu().numpy() - o.flat("critic")).max()
     assert dc <= 5e-4 * 20, dc
+
+
+def test_coma_chain_failure_is_loud(monkeypatch):
+    """A persistent-chain workgroup that stops flagging (MQ_COMA_CHAIN_FAULT test hook) makes every workgroup leave
+    within the bounded spin: the launch ends, the stats come out NaN with critic_steps = -1 and train() raises;
+    the next train() runs normally."""
+    from tests.gpu_helpers import build_coma
+    from pymarl_amd._lib import MQError
+    monkeypatch.delenv("MQ_COMA_CHAIN", raising=False)
+    c = get({}, "coma_tiny")
+    args, buf, mac, learner, logger = build_coma(c)
+    np.random.seed(c.sampler_seed)
+    batch = buf.sample(c.B)
+    batch = batch[:, :batch.max_t_filled()]
+    mac.action_selector.epsilon = c.epsilon[0]
+    monkeypatch.setenv("MQ_COMA_CHAIN_FAULT", "1")
+    with pytest.raises(MQError):
+        learner.train(batch, 1000, 0)
+    assert learner.critic_path() == "chain"
+    assert np.isnan(learner._stats[0].item())
+    monkeypatch.delenv("MQ_COMA_CHAIN_FAULT")
+    learner.train(batch, 2000, 8)
+    st = learner.last_stats()
+    assert st["critic_steps"] > 0 and np.isfinite(st["critic_loss"])
