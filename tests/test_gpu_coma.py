@@ -246,3 +246,27 @@ def test_coma_chain_failure_is_loud(monkeypatch):
     learner.train(batch, 2000, 8)
     st = learner.last_stats()
     assert st["critic_steps"] > 0 and np.isfinite(st["critic_loss"])
+
+
+def test_coma_chain_bitwise_deterministic(coma_cases, monkeypatch):
+    """The persistent chain has no data atomics and sums every reduction in a fixed order: two train() calls from
+    the same state on the same batch give bitwise-identical critic parameters, square_avg and stats."""
+    from oracle.coma_np import OracleCOMALearner
+    from tests.gpu_helpers import build_coma
+    monkeypatch.delenv("MQ_COMA_CHAIN", raising=False)
+    c = get(coma_cases, "coma_cfg5")
+    args, buf, mac, learner, logger = build_coma(c)
+    o = OracleCOMALearner(c.agent_params, c.critic_params, c.cfg())
+    np.random.seed(c.sampler_seed)
+    batch = buf.sample(c.B)
+    batch = batch[:, :batch.max_t_filled()]
+    outs = []
+    for _ in range(2):
+        load_state(learner, o)
+        mac.action_selector.epsilon = c.epsilon[0]
+        learner.train(batch, 1000, 0)
+        assert learner.critic_path() == "chain"
+        outs.append((learner._critic.cpu().numpy().copy(), learner._csq.cpu().numpy().copy(),
+                     learner._stats.cpu().numpy().copy()))
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b)
