@@ -303,6 +303,44 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
     MQ_HIP(hipMemcpyAsync(h->dp_msum.data(), h->msum, (size_t)T * sizeof(float), hipMemcpyDeviceToHost, s));
     MQ_HIP(hipStreamSynchronize(s));
   }
+  // ---- the actor's agent unroll over t < T (coma_learner.py:52-57), online net only. It reads nothing the critic
+  // writes, so beside the persistent chain it runs on the side stream in the CUs the chain leaves idle.
+  mq_replay av = *batch;
+  av.t_len = T;
+  Dims d = make_dims(ah, &av);
+  const Lay L = make_lay(ah);
+  Work w = ah->w;
+  w.dHo = h->dHo;
+  const int64_t RT = (int64_t)T * R;
+  const float* Pa = h->agent;
+  auto agent_forward = [&](hipStream_t st) -> int {
+    const int rw_fwd = pick_rw(d.R, 512);
+    if (rw_fwd == 1 && fused_fwd_ok(d.I, d.O, d.A, d.n, RT)) {
+      launch_fwd_fused(dim3(d.R, 1), st, d, rp, Pa, Pa, L, w);
+      MQ_HIP(hipGetLastError());
+    } else {
+      Fc1Prob p1{d, rp, Pa, Pa, ah->off[MQ_P_FC1_W], ah->off[MQ_P_FC1_B], w.X1, w.XIN, RT};
+      MQ_HIP(launch_gemm(p1, (int)RT, 2 * mq::H, 1, st));
+      GiProb p2{w.X1, Pa, Pa, ah->off[MQ_P_RNN_W_IH], ah->off[MQ_P_RNN_B_IH], w.GI, RT};
+      MQ_HIP(launch_gemm(p2, (int)RT, mq::G3, 1, st));
+      const dim3 grid((d.R + rw_fwd - 1) / rw_fwd, 1);
+      if (rw_fwd == 1) hipLaunchKernelGGL((gru_fwd_kernel<1, 0>), grid, dim3(256), 0, st, d, Pa, Pa, L, w);
+      else if (rw_fwd == 2) hipLaunchKernelGGL((gru_fwd_kernel<2, 0>), grid, dim3(256), 0, st, d, Pa, Pa, L, w);
+      else if (rw_fwd == 4) hipLaunchKernelGGL((gru_fwd_kernel<4, 0>), grid, dim3(256), 0, st, d, Pa, Pa, L, w);
+      else hipLaunchKernelGGL((gru_fwd_kernel<8, 0>), grid, dim3(256), 0, st, d, Pa, Pa, L, w);
+      MQ_HIP(hipGetLastError());
+      Fc2Prob p3{w.Hs, Pa, Pa, ah->off[MQ_P_FC2_W], ah->off[MQ_P_FC2_B], w.Q, RT, d.A};
+      MQ_HIP(launch_gemm(p3, (int)RT, d.A, 1, st));
+    }
+    return MQ_OK;
+  };
+  const char* ov = std::getenv("MQ_COMA_OVERLAP");
+  const bool try_overlap = !dp && !h->timing && !(ov && ov[0] == '0') && h->chain_env && cc_ok(R, A, h->Kc, h->num_cu);
+  if (try_overlap) {
+    MQ_HIP(ensure_side(ah));
+    MQ_HIP(hipEventRecord(ah->ev_fork, s));   // before the chain: the side stream does not wait for it
+  }
+  bool actor_side = false;
   if (h->timing) MQ_HIP(hipEventRecord(h->ev[1], s));
   bool chained = false;
   if (!dp && h->chain_env && cc_ok(R, A, h->Kc, h->num_cu)) {   // every critic step in one cooperative launch
@@ -348,6 +386,12 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
       (void)hipGetLastError();
       h->chain_env = false;
     }
+    if (chained && try_overlap) {   // launched after the chain, so the chain's workgroups are dispatched first
+      MQ_HIP(hipStreamWaitEvent(ah->side, ah->ev_fork, 0));
+      if ((rc = agent_forward(ah->side)) != MQ_OK) return rc;
+      MQ_HIP(hipEventRecord(ah->ev_join, ah->side));
+      actor_side = true;
+    }
   }
   int live = 0;
   for (int t = T - 1; t >= 0 && !chained; --t) {
@@ -378,33 +422,9 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   }
 
   if (h->timing) MQ_HIP(hipEventRecord(h->ev[2], s));
-  // ---- actor: the agent unroll over t < T (coma_learner.py:52-57), online net only
-  mq_replay av = *batch;
-  av.t_len = T;
-  Dims d = make_dims(ah, &av);
-  const Lay L = make_lay(ah);
-  Work w = ah->w;
-  w.dHo = h->dHo;
-  const int64_t RT = (int64_t)T * R;
-  const float* Pa = h->agent;
-  const int rw_fwd = pick_rw(d.R, 512);
-  if (rw_fwd == 1 && fused_fwd_ok(d.I, d.O, d.A, d.n, RT)) {
-    launch_fwd_fused(dim3(d.R, 1), s, d, rp, Pa, Pa, L, w);
-    MQ_HIP(hipGetLastError());
-  } else {
-    Fc1Prob p1{d, rp, Pa, Pa, ah->off[MQ_P_FC1_W], ah->off[MQ_P_FC1_B], w.X1, w.XIN, RT};
-    MQ_HIP(launch_gemm(p1, (int)RT, 2 * mq::H, 1, s));
-    GiProb p2{w.X1, Pa, Pa, ah->off[MQ_P_RNN_W_IH], ah->off[MQ_P_RNN_B_IH], w.GI, RT};
-    MQ_HIP(launch_gemm(p2, (int)RT, mq::G3, 1, s));
-    const dim3 grid((d.R + rw_fwd - 1) / rw_fwd, 1);
-    if (rw_fwd == 1) hipLaunchKernelGGL((gru_fwd_kernel<1, 0>), grid, dim3(256), 0, s, d, Pa, Pa, L, w);
-    else if (rw_fwd == 2) hipLaunchKernelGGL((gru_fwd_kernel<2, 0>), grid, dim3(256), 0, s, d, Pa, Pa, L, w);
-    else if (rw_fwd == 4) hipLaunchKernelGGL((gru_fwd_kernel<4, 0>), grid, dim3(256), 0, s, d, Pa, Pa, L, w);
-    else hipLaunchKernelGGL((gru_fwd_kernel<8, 0>), grid, dim3(256), 0, s, d, Pa, Pa, L, w);
-    MQ_HIP(hipGetLastError());
-    Fc2Prob p3{w.Hs, Pa, Pa, ah->off[MQ_P_FC2_W], ah->off[MQ_P_FC2_B], w.Q, RT, d.A};
-    MQ_HIP(launch_gemm(p3, (int)RT, d.A, 1, s));
-  }
+  // ---- actor: the agent unroll over t < T (coma_learner.py:52-57), online net only (launched above)
+  if (actor_side) MQ_HIP(hipStreamWaitEvent(s, ah->ev_join, 0));
+  else if ((rc = agent_forward(s)) != MQ_OK) return rc;
   // policy, baseline, advantage, loss sums and dLogits (coma_learner.py:59-77, basic_controller.py:53-73)
   const int npol = (int)((RT + 3) / 4);
   const float eps = epsilon, omeps = (float)(1.0 - (double)epsilon);
