@@ -109,11 +109,11 @@ int mc_critic_forward(const float* critic, const mc_config* cfg, const mq_replay
                 o_w3 = o_b2 + CH, o_b3 = o_w3 + (int64_t)A * CH;
   hipLaunchKernelGGL(coma_xin_kernel, dim3((unsigned)M), dim3(256), 0, s, cd, rp, X, t0);
   MQ_HIP(hipGetLastError());
-  CLinProb l1{X, cd.Kp, critic + o_w1, critic + o_b1, H1, M, CH, cd.Kc, 1};
+  const CLinProbT<64> l1 = CLinProbT<64>{X, cd.Kp, critic + o_w1, critic + o_b1, H1, M, CH, cd.Kc, 1}.with_vec();
   MQ_HIP(launch_gemm(l1, (int)M, CH, 1, s));
-  CLinProb l2{H1, CH, critic + o_w2, critic + o_b2, H2, M, CH, CH, 1};
+  const CLinProbT<64> l2 = CLinProbT<64>{H1, CH, critic + o_w2, critic + o_b2, H2, M, CH, CH, 1}.with_vec();
   MQ_HIP(launch_gemm(l2, (int)M, CH, 1, s));
-  CLinProb l3{H2, CH, critic + o_w3, critic + o_b3, Q, M, A, CH, 0};
+  const CLinProbT<64> l3 = CLinProbT<64>{H2, CH, critic + o_w3, critic + o_b3, Q, M, A, CH, 0}.with_vec();
   MQ_HIP(launch_gemm(l3, (int)M, A, 1, s));
   const int64_t tot = M * A;
   hipLaunchKernelGGL(coma_q_layout_kernel, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, 4096)), dim3(256), 0, s,
@@ -268,11 +268,15 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   {
     const int64_t M = (int64_t)Tp * R;
     const float* tc = h->tcritic;
-    CLinProb l1{h->X, h->Kp, tc + h->coff[MC_P_FC1_W], tc + h->coff[MC_P_FC1_B], h->H1t, M, CH, h->Kc, 1};
+    const CLinProbT<64> l1 =
+        CLinProbT<64>{h->X, h->Kp, tc + h->coff[MC_P_FC1_W], tc + h->coff[MC_P_FC1_B], h->H1t, M, CH, h->Kc, 1}
+            .with_vec();
     MQ_HIP(launch_gemm(l1, (int)M, CH, 1, s));
-    CLinProb l2{h->H1t, CH, tc + h->coff[MC_P_FC2_W], tc + h->coff[MC_P_FC2_B], h->H2t, M, CH, CH, 1};
+    const CLinProbT<64> l2 =
+        CLinProbT<64>{h->H1t, CH, tc + h->coff[MC_P_FC2_W], tc + h->coff[MC_P_FC2_B], h->H2t, M, CH, CH, 1}.with_vec();
     MQ_HIP(launch_gemm(l2, (int)M, CH, 1, s));
-    CLinProb l3{h->H2t, CH, tc + h->coff[MC_P_FC3_W], tc + h->coff[MC_P_FC3_B], h->Qt, M, A, CH, 0};
+    const CLinProbT<64> l3 =
+        CLinProbT<64>{h->H2t, CH, tc + h->coff[MC_P_FC3_W], tc + h->coff[MC_P_FC3_B], h->Qt, M, A, CH, 0}.with_vec();
     MQ_HIP(launch_gemm(l3, (int)M, A, 1, s));
   }
   const size_t lds_td = (size_t)Tp * (n + 3) * sizeof(float);

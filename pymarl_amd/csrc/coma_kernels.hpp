@@ -94,8 +94,10 @@ __global__ __launch_bounds__(256) void coma_mask_kernel(CDims d, Rep rp, float* 
 }
 
 // Dense linear layer for the target critic's all-steps forward: out[m][j] = act(X[m][:K] . W[j][:K] + bias[j]).
-struct CLinProb {
-  static constexpr int BN = 128;
+// BN_ = 64 for the wide-K layer: twice the workgroups (two per CU at cfg5) for latency hiding
+template <int BN_ = 128>
+struct CLinProbT {
+  static constexpr int BN = BN_;
   const float* X;   // [M][ldx]
   int ldx;
   const float* W;   // [N][K] row-major (the reference layout)
@@ -103,6 +105,13 @@ struct CLinProb {
   float* out;       // [M][N]
   int64_t M;
   int N, K, relu;
+  bool vec_a = false, vec_b = false;   // set by with_vec(): 16-B aligned rows
+  CLinProbT with_vec() const {
+    CLinProbT q = *this;
+    q.vec_a = ldx % 4 == 0 && ((uintptr_t)X & 15) == 0;
+    q.vec_b = K % 4 == 0 && ((uintptr_t)W & 15) == 0;
+    return q;
+  }
   using APat = KPat;
   using BPat = KPat;
   static constexpr bool kRowSum = false;
@@ -122,14 +131,26 @@ struct CLinProb {
     return c;
   }
   MQ_DEV void krange(int, int& kb, int& ke) const { kb = 0; ke = K; }
+  // 16-B loads where the 4-run is inside K (rows are 16-B aligned: ldx and K are multiples of 4 wherever the
+  // vector path is taken, checked by vec_ok), element loads at the K tail
   MQ_DEV void load_a(const Ctx& c, int k0, int ke, float (&r)[4]) const {
     const int k = k0 + KPat::kq(threadIdx.x);
+    if (c.arow && vec_a && k + 3 < ke) {
+      const f32x4 v = *(const f32x4*)&c.arow[k];
+      r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; r[3] = v[3];
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) r[i] = (c.arow && k + i < ke) ? c.arow[k + i] : 0.0f;
   }
   MQ_DEV void load_b(const Ctx& c, int pass, int k0, int ke, float (&r)[4]) const {
     const int k = k0 + KPat::kq(threadIdx.x);
     const float* p = c.brow[pass];
+    if (p && vec_b && k + 3 < ke) {
+      const f32x4 v = *(const f32x4*)&p[k];
+      r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; r[3] = v[3];
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) r[i] = (p && k + i < ke) ? p[k + i] : 0.0f;
   }
@@ -146,6 +167,7 @@ struct CLinProb {
   }
   MQ_DEV void rowsum_out(int, int, float) const {}
 };
+using CLinProb = CLinProbT<128>;
 
 // build_td_lambda_targets (rl_utils.py:4-14), one workgroup per episode: the recursion's inputs (the target critic's
 // Q at the taken action for every (t, agent), reward, terminated, mask) are gathered into LDS by all threads, then
