@@ -81,3 +81,21 @@ def test_train_without_handle_bound_reports_state_error():
     assert lib.mq_apply(None, None) != 0
     assert lib.mq_forward_backward(None, None, None) != 0
     assert lib.mq_last_plan(None, ctypes.byref(_lib.MQPlan())) != 0
+
+
+def test_coma_host_only_entry_points():
+    """COMA entry points that need no GPU: the critic-path query before any handle, the standalone critic
+    forward's workspace size (coma.py:61-70 input width, include/mc_coma.h), and its argument checks."""
+    lib = _lib.load()
+    assert lib.mc_last_critic_path(None) == -1
+    n, A, O, S = 10, 18, 176, 322
+    cfg = _lib.MCConfig(n_agents=n, n_actions=A, obs_dim=O, state_dim=S, rnn_hidden_dim=64, obs_last_action=1,
+                        obs_agent_id=1, max_batch=8, max_seq=181)
+    B, Tq = 8, 181
+    ws = lib.mc_critic_forward_workspace(ctypes.byref(cfg), B, Tq)
+    Kc = S + O + 2 * n * A + n
+    M = Tq * B * n
+    assert ws >= M * ((Kc + 3) // 4 * 4) + 2 * M * 128 + M * A
+    assert lib.mc_critic_forward_workspace(ctypes.byref(cfg), 0, Tq) == -1
+    assert lib.mc_critic_forward(None, ctypes.byref(cfg), None, 0, None, None, None) != 0
+    assert b"NULL" in lib.mq_last_error()
