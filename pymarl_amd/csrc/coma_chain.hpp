@@ -13,7 +13,7 @@
 //   C  (all)   dW1 tile = dH1[:, units]^T X_t[:, K slice] (registers), db1 (ks = 0), the 64 dW2 16x16 tiles and
 //              the dW3 tiles round-robin over the workgroups, per-workgroup sum of squares
 //   D  (all)   the global gradient norm from the G partials (fixed order), clip coefficient, RMSprop on the owned
-//              W1 tile and on the owned slice of fc1.bias .. fc3.bias; workgroup 0 records the stats
+//              W1 tile and on the owned slice of fc1.bias .. fc3.bias; the last workgroup records the stats
 // The hand-offs are flags, not grid barriers: A -> B every workgroup flags, only the heads wait; B -> C the heads
 // flag, every workgroup waits; C -> D each workgroup publishes its sum of squares as one 8-B {value, step tag}
 // granule after draining its stores, and every workgroup's wave 0 polls all G granules. Buffers reused by the next
@@ -630,7 +630,6 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
     // Valid forms: R2 granules / row 1 flags), and the other waves join behind the workgroup barrier below
     stamp(6);
     // ================================================================ D: clip + RMSprop (coma_learner.py:132-134)
-    float* np_s = H1s;   // head scratch is dead in phase D: workgroup 0's copy of the loss partials
     if (w == 0) {   // the squared norm: each lane sums its partials (lane, lane + 64, ..), then a fixed butterfly
       float pv[4];
       const unsigned tag = (unsigned)(live + 1);
@@ -666,8 +665,16 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
         misc[49] = fminf(a.hp.clip / (norm + 1e-6f), 1.0f);
         misc[50] = norm;
       }
-    } else if (w == 1 && wg == 0) {   // written in phase B: ordered by barrier 2
-      if (lane < 8 * a.NHEAD) np_s[256 + lane] = ld_wt(&a.part[lane]);
+    } else if (w == 1 && wg == a.NG - 1 && lane < 8) {   // the step's critic stats (coma_learner.py:136-139), off
+      // workgroup 0's path (a head): lane k sums loss partial k over the heads in head order (written in phase B,
+      // ordered by the B -> C flags)
+      const int k = lane;
+      float s = 0.0f;
+      for (int h = 0; h < a.NHEAD; ++h) s += ld_wt(&a.part[h * 8 + k]);
+      float* rec = a.crec + t * 8;
+      if (k == 0 || k == 2 || k == 3 || k == 4) rec[k] = s;
+      else if (k == 1) rec[1] = mt;
+      else if (k == 6) rec[6] = 1.0f;
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the exchanged-data loads below the poll
@@ -694,18 +701,7 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
       a.SQ[i] = v;
       a.G[i] = gg;   // the last live step's clipped gradient stays
     }
-    if (wg == 0 && tid == 0) {   // the step's critic stats (coma_learner.py:136-139)
-      float* rec = a.crec + t * 8;
-      for (int k = 0; k < 5; ++k) {
-        if (k == 1) continue;
-        float s = 0.0f;
-        for (int h = 0; h < a.NHEAD; ++h) s += np_s[256 + h * 8 + k];
-        rec[k] = s;
-      }
-      rec[1] = mt;
-      rec[5] = misc[50];
-      rec[6] = 1.0f;
-    }
+    if (wg == a.NG - 1 && tid == 0) a.crec[t * 8 + 5] = misc[50];   // the step's gradient norm
     stamp(7);
     ++live;
     last_t = t;
