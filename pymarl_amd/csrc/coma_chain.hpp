@@ -68,7 +68,7 @@ MQ_DEV f32x4 ld_wt4(const float* p) {
   asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
   return v;
 }
-// 16-B write-through store (global_store_dwordx4 sc1); drained by the grid barrier's vmcnt(0) like every store
+// 16-B write-through store (global_store_dwordx4 sc1); drained by cc_post's vmcnt(0) like every store
 MQ_DEV void st_wt4(float* p, f32x4 v) { asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(v) : "memory"); }
 MQ_DEV void cc_vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 MQ_DEV void cc_ready(f32x4& v) { asm volatile("" : "+v"(v)); }
