@@ -90,6 +90,9 @@ int32_t mc_last_critic_path(const mc_handle* h);
  * host reads the global mask sums back once per train (one synchronisation) to know the live steps.
  * `scratch` holds >= 8 * max_seq floats. allreduce = NULL switches data parallelism off. */
 typedef int (*mc_allreduce_fn)(float* buf, int64_t count, void* stream, void* ctx);
+/* The same exchange steps over a native RCCL communicator (id from mq_comm_unique_id, one process per GPU): no
+ * host callback per critic step. Replaces any mc_set_data_parallel callback; scratch is library-owned. */
+int mc_comm_attach(mc_handle* h, const uint8_t* id, int32_t rank, int32_t world);
 int mc_set_data_parallel(mc_handle* h, mc_allreduce_fn allreduce, void* ctx, int32_t rank, float* scratch,
                          int64_t scratch_count);
 /* 0 = critic Q values the actor used [T][B*n][A]; 1 = TD(lambda) targets [T][B*n]; 2 = policy pi [T][B*n][A]. */

@@ -96,6 +96,18 @@ int mq_train_step(mq_handle* h, const mq_replay* batch, void* stream);
 /* Declare that the caller sums the gradient buffer across ranks between mq_forward_backward and mq_apply
  * (mq_apply then recomputes the global gradient norm from the reduced buffer). */
 int mq_set_data_parallel(mq_handle* h, int32_t on);
+/* Native RCCL data parallelism (SURVEY.md §8b's mq_allreduce_attach): rank 0 calls mq_comm_unique_id and ships
+ * the MQ_COMM_ID_BYTES bytes to every rank over any channel; every rank (one process per GPU) then calls
+ * mq_comm_attach(h, id, rank, world) once. From then on mq_forward_backward ends with one RCCL all-reduce (sum) of
+ * the whole grad buffer [P + MQ_NSUMS] on `stream`, and mq_apply recomputes the norm from the sum: one call of
+ * mq_train_step is a full data-parallel QLearner.train step, with no host collective in between. world = 1 is
+ * allowed (the all-reduce is the identity). mq_comm_world reports the attached world size (0: none);
+ * mq_comm_detach frees the communicator (mq_destroy does too). */
+enum { MQ_COMM_ID_BYTES = 128 };
+int mq_comm_unique_id(uint8_t* id /* [MQ_COMM_ID_BYTES] */);
+int mq_comm_attach(mq_handle* h, const uint8_t* id, int32_t rank, int32_t world);
+int32_t mq_comm_world(const mq_handle* h);
+int mq_comm_detach(mq_handle* h);
 int mq_update_targets(mq_handle* h, void* stream);
 
 /* Copy an intermediate of the last mq_forward_backward into dst (device): 0 = online mac_out [t][b*n+a][A],

@@ -29,7 +29,8 @@ EXPORTS = [
     "mq_last_plan", "mq_qmix_forward",
     # include/mc_coma.h
     "mc_create", "mc_destroy", "mc_param_offsets", "mc_bind", "mc_train_step", "mc_update_targets", "mc_policy",
-    "mc_copy_intermediate", "mc_set_timing", "mc_phase_times", "mc_last_critic_path", "mc_set_data_parallel", "mc_critic_forward",
+    "mc_copy_intermediate", "mc_set_timing", "mc_phase_times", "mc_last_critic_path", "mq_comm_unique_id", "mq_comm_attach",
+    "mq_comm_world", "mq_comm_detach", "mc_comm_attach", "mc_set_data_parallel", "mc_critic_forward",
     "mc_critic_forward_workspace",
 ]
 
@@ -141,6 +142,11 @@ def load(required=True):
         "mc_set_timing": ([vp, i32], ctypes.c_int),
         "mc_phase_times": ([vp, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         "mc_last_critic_path": ([vp], i32),
+        "mq_comm_unique_id": ([vp], ctypes.c_int),
+        "mq_comm_attach": ([vp, vp, i32, i32], ctypes.c_int),
+        "mq_comm_world": ([vp], i32),
+        "mq_comm_detach": ([vp], ctypes.c_int),
+        "mc_comm_attach": ([vp, vp, i32, i32], ctypes.c_int),
         "mc_set_data_parallel": ([vp, MC_ALLREDUCE_FN, vp, i32, vp, i64], ctypes.c_int),
     }
     for name, (args, res) in sig.items():

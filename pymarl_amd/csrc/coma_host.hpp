@@ -36,6 +36,8 @@ struct mc_handle {
   float* dp_scratch = nullptr;
   int64_t dp_scratch_n = 0;
   std::vector<float> dp_msum;
+  ncclComm_t comm = nullptr;   // mc_comm_attach: native RCCL exchange steps
+  float* comm_scratch = nullptr;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -206,6 +208,8 @@ int mc_destroy(mc_handle* h) {
   if (!h) return MQ_OK;
   if (h->ws) (void)hipFree(h->ws);
   if (h->chain_trace) (void)hipFree(h->chain_trace);
+  if (h->comm) (void)ncclCommDestroy(h->comm);
+  if (h->comm_scratch) (void)hipFree(h->comm_scratch);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
   mq_destroy(h->ah);
@@ -524,6 +528,22 @@ int mc_set_data_parallel(mc_handle* h, mc_allreduce_fn allreduce, void* ctx, int
   h->dp_scratch = scratch;
   h->dp_scratch_n = scratch_count;
   return MQ_OK;
+}
+
+// mc_allreduce_fn over the handle's RCCL communicator (ctx = the mc_handle)
+static int mc_rccl_allreduce(float* buf, int64_t count, void* stream, void* ctx) {
+  mc_handle* h = (mc_handle*)ctx;
+  return ncclAllReduce(buf, buf, (size_t)count, ncclFloat, ncclSum, h->comm, (hipStream_t)stream) == ncclSuccess ? 0 : 1;
+}
+
+int mc_comm_attach(mc_handle* h, const uint8_t* id, int32_t rank, int32_t world) {
+  if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
+  if (h->comm) return set_err(MQ_ERR_STATE, "a communicator is already attached");
+  const int64_t n = 8LL * h->cfg.max_seq;
+  if (!h->comm_scratch) MQ_HIP(hipMalloc(&h->comm_scratch, n * sizeof(float)));
+  const int rc = comm_init(&h->comm, id, rank, world);
+  if (rc) return rc;
+  return mc_set_data_parallel(h, mc_rccl_allreduce, h, rank, h->comm_scratch, n);
 }
 
 int mc_set_timing(mc_handle* h, int32_t on) {

@@ -22,6 +22,7 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
 #include "learner_gemms.hpp"
 #include "gru_kernels.hpp"
 #include "gru_fwd_fused.hpp"
@@ -90,6 +91,8 @@ struct mq_handle {
   int dwh_split = getenv("MQ_DWH_SPLIT") ? atoi(getenv("MQ_DWH_SPLIT")) : 8;   // m-slices of the dW_hyper pass
   bool generic_mix = getenv("MQ_GENERIC_MIX") != nullptr;   // A/B switch: mix_kernel instead of mix_fast_kernel
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
+  ncclComm_t comm = nullptr;   // mq_comm_attach: the library all-reduces the grad buffer itself
+  int comm_world = 0;
   // A/B switch, off by default: dW_hyper on a side stream beside the fused BPTT (dwh_kernel.hpp). Measured at cfg2
   // (r01l): the co-resident dwh_side waves slow the BPTT chain 92.7 -> 105.6 us, the step 238 -> 264 us
   bool dwh_overlap = getenv("MQ_DWH_OVERLAP") && atoi(getenv("MQ_DWH_OVERLAP")) != 0;
@@ -381,6 +384,7 @@ int mq_destroy(mq_handle* h) {
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->side) (void)hipStreamDestroy(h->side);
   if (h->ws) (void)hipFree(h->ws);
+  if (h->comm) (void)ncclCommDestroy(h->comm);
   delete h;
   return MQ_OK;
 }
@@ -605,6 +609,10 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
     h->n_norm_part = rb.b2;
   }
   pt.end();
+  if (h->comm) {   // native data parallelism: the whole [grads | sums] buffer, summed over the ranks in stream order
+    const ncclResult_t r = ncclAllReduce(h->grad, h->grad, (size_t)(h->P + MQ_NSUMS), ncclFloat, ncclSum, h->comm, s);
+    if (r != ncclSuccess) return set_err(MQ_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  }
   h->last = d;
   h->plan = plan;
   h->have_fb = true;
@@ -617,7 +625,7 @@ int mq_apply(mq_handle* h, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   PhaseTimer pt{h, s};
   pt.begin(PH_APPLY);
-  if (h->dp) {   // the gradient was all-reduced after the reduce pass: its norm partials are stale
+  if (h->dp || h->comm) {   // the gradient was all-reduced after the reduce pass: its norm partials are stale
     h->n_norm_part = 256;
     hipLaunchKernelGGL(sumsq_kernel, dim3(h->n_norm_part), dim3(256), 0, s, (const float*)h->grad, h->P,
                        h->w.norm_part);
@@ -643,6 +651,45 @@ int mq_last_plan(const mq_handle* h, mq_plan* out) {
 int mq_set_data_parallel(mq_handle* h, int32_t on) {
   if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
   h->dp = on != 0;
+  return MQ_OK;
+}
+
+int mq_comm_unique_id(uint8_t* id) {
+  if (!id) return set_err(MQ_ERR_ARG, "NULL id");
+  ncclUniqueId u;
+  const ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return set_err(MQ_ERR_HIP, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  static_assert(sizeof(u) == MQ_COMM_ID_BYTES, "ncclUniqueId size");
+  std::memcpy(id, &u, sizeof(u));
+  return MQ_OK;
+}
+
+// One RCCL communicator over `world` ranks (the calling process's current HIP device).
+static int comm_init(ncclComm_t* out, const uint8_t* id, int32_t rank, int32_t world) {
+  if (!id || world < 1 || rank < 0 || rank >= world) return set_err(MQ_ERR_ARG, "mq_comm_attach: bad id, rank or world");
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  const ncclResult_t r = ncclCommInitRank(out, world, u, rank);
+  if (r != ncclSuccess) return set_err(MQ_ERR_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  return MQ_OK;
+}
+
+int mq_comm_attach(mq_handle* h, const uint8_t* id, int32_t rank, int32_t world) {
+  if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
+  if (h->comm) return set_err(MQ_ERR_STATE, "a communicator is already attached (mq_comm_detach first)");
+  const int rc = comm_init(&h->comm, id, rank, world);
+  if (rc) return rc;
+  h->comm_world = world;
+  return MQ_OK;
+}
+
+int32_t mq_comm_world(const mq_handle* h) { return h ? h->comm_world : 0; }
+
+int mq_comm_detach(mq_handle* h) {
+  if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
+  if (h->comm) (void)ncclCommDestroy(h->comm);
+  h->comm = nullptr;
+  h->comm_world = 0;
   return MQ_OK;
 }
 
