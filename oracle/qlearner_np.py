@@ -52,20 +52,25 @@ def _elu(x):
     return np.where(x > 0, x, np.expm1(np.minimum(x, F32(0.0)))).astype(F32)
 
 
-def build_inputs(obs_t, onehot_prev, n_agents):
-    """basic_controller.py:100-135: cat[obs_t, onehot(a_{t-1}) (0 at t=0), eye(n)] -> (B*n, I)."""
+def build_inputs(obs_t, onehot_prev, n_agents, flags=(True, True)):
+    """basic_controller.py:100-135: cat[obs_t, onehot(a_{t-1}) (0 at t=0) if obs_last_action (:111-116),
+    eye(n) if obs_agent_id (:118-120)] -> (B*n, I). flags = (obs_last_action, obs_agent_id)."""
     B = obs_t.shape[0]
-    eye = np.broadcast_to(np.eye(n_agents, dtype=F32), (B, n_agents, n_agents))
-    return np.concatenate([obs_t, onehot_prev, eye], -1).reshape(B * n_agents, -1).astype(F32)
+    parts = [obs_t]
+    if flags[0]:
+        parts.append(onehot_prev)
+    if flags[1]:
+        parts.append(np.broadcast_to(np.eye(n_agents, dtype=F32), (B, n_agents, n_agents)))
+    return np.concatenate(parts, -1).reshape(B * n_agents, -1).astype(F32)
 
 
-def agent_unroll(p, obs, actions_onehot, keep_cache=False, relu_mask=None, pre_out=None):
+def agent_unroll(p, obs, actions_onehot, keep_cache=False, relu_mask=None, pre_out=None, flags=(True, True)):
     """BasicMAC.forward over t = 0..T (q_learner.py:47-52 / 58-62) with RNNAgent (rnn_agent.py:27-36).
 
     obs (B,Tp,n,O), actions_onehot (B,Tp,n,A) -> mac_out (B,Tp,n,A) [+ cache for the backward pass].
     relu_mask (B,Tp,n,H) bool: take the fc1 relu's on/off decisions from another implementation (a parity test
     following it through fc1 pre-activations that round to the other side of 0). pre_out: list receiving the
-    fc1 pre-activations per step.
+    fc1 pre-activations per step. flags: (obs_last_action, obs_agent_id), basic_controller.py:111-120.
     """
     B, Tp, n, _ = obs.shape
     A = actions_onehot.shape[-1]
@@ -74,7 +79,7 @@ def agent_unroll(p, obs, actions_onehot, keep_cache=False, relu_mask=None, pre_o
     outs, cache = [], []
     for t in range(Tp):
         prev = np.zeros((B, n, A), F32) if t == 0 else actions_onehot[:, t - 1]
-        x = build_inputs(obs[:, t], prev, n)
+        x = build_inputs(obs[:, t], prev, n, flags)
         pre = x @ p["fc1.weight"].T + p["fc1.bias"]
         if pre_out is not None:
             pre_out.append(pre.reshape(B, n, -1))
@@ -94,14 +99,14 @@ def agent_unroll(p, obs, actions_onehot, keep_cache=False, relu_mask=None, pre_o
     return np.stack(outs, 1).astype(F32), cache
 
 
-def fc1_preacts(p, obs, actions_onehot):
+def fc1_preacts(p, obs, actions_onehot, flags=(True, True)):
     """fc1 pre-activations of every (b, t, agent) (rnn_agent.py:28 before the relu): (B,Tp,n,H)."""
     B, Tp, n, _ = obs.shape
     A = actions_onehot.shape[-1]
     out = []
     for t in range(Tp):
         prev = np.zeros((B, n, A), F32) if t == 0 else actions_onehot[:, t - 1]
-        x = build_inputs(obs[:, t], prev, n)
+        x = build_inputs(obs[:, t], prev, n, flags)
         out.append((x @ p["fc1.weight"].T + p["fc1.bias"]).reshape(B, n, -1))
     return np.stack(out, 1).astype(F32)
 
@@ -215,6 +220,11 @@ class OracleQLearner:
         self.log_stats_t = -self.cfg.get("learner_log_interval", 0) - 1
         self.last = {}
 
+    @property
+    def input_flags(self):
+        """(obs_last_action, obs_agent_id): basic_controller.py:111,118 (True / True in every shipped config)."""
+        return (bool(self.cfg.get("obs_last_action", True)), bool(self.cfg.get("obs_agent_id", True)))
+
     def forward(self, batch, keep_cache=False, cur_max_override=None, relu_override=None):
         """q_learner.py:39-97: returns dict of intermediates (+ caches).
 
@@ -230,9 +240,11 @@ class OracleQLearner:
         mask = batch["filled"][:, :-1].astype(F32).copy()
         mask[:, 1:] = mask[:, 1:] * (F32(1.0) - terminated[:, :-1])
         avail = batch["avail_actions"]
-        mac_out, acache = agent_unroll(self.p, batch["obs"], batch["actions_onehot"], keep_cache, relu_override)
+        fl = self.input_flags
+        mac_out, acache = agent_unroll(self.p, batch["obs"], batch["actions_onehot"], keep_cache, relu_override,
+                                       flags=fl)
         chosen = np.take_along_axis(mac_out[:, :-1], actions, axis=3)[..., 0]
-        tmo_full, _ = agent_unroll(self.tp, batch["obs"], batch["actions_onehot"])
+        tmo_full, _ = agent_unroll(self.tp, batch["obs"], batch["actions_onehot"], flags=fl)
         tmo = tmo_full[:, 1:].copy()
         tmo[avail[:, 1:] == 0] = NEG
         if c.get("double_q", True):
@@ -242,8 +254,10 @@ class OracleQLearner:
             if cur_max_override is not None:
                 cur_max = np.asarray(cur_max_override, dtype=np.int64)
             target_max = np.take_along_axis(tmo, cur_max[..., None], axis=3)[..., 0]
-        else:
+        else:   # q_learner.py:77-78: target_mac_out.max(dim=3); argmax kept for the decision accounting
             cur_max = tmo.argmax(axis=3)
+            if cur_max_override is not None:
+                cur_max = np.asarray(cur_max_override, dtype=np.int64)
             target_max = tmo.max(axis=3)
         mcache = None
         if c["mixer"] == "qmix":

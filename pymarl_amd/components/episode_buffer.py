@@ -12,6 +12,10 @@ MI355X-first differences (behaviour-preserving for the learner):
   would.
 * Episode lengths are tracked on the host at insert time, so `SampledBatch.max_t_filled()` is a host max (no
   device sync); the result equals the reference's `sum(filled, 1).max(0)`.
+* A host-resident buffer (`buffer_cpu_only: True`, run.py:137-139) keeps the reference's flow: `sample` ->
+  `[:, :max_t]` -> `.to(args.device)` in place (run.py:208-215). `SampledBatch.to` then gathers the sampled episodes
+  on the host and copies each field to the device once; the batch is dense from then on (`dense`), and the learner
+  reads it through the dense (no episode id) kernel path.
 """
 from __future__ import annotations
 
@@ -185,8 +189,26 @@ class EpisodeBatch:
             self.batch_size, self.max_seq_length, self.scheme.keys(), self.groups.keys())
 
 
+def _same_device(a, b):
+    a, b = th.device(a), th.device(b)
+    if a.type != b.type:
+        return False
+    if a.type != "cuda" or a.index == b.index:
+        return True
+    cur = th.cuda.current_device() if th.cuda.is_available() else 0
+    return (cur if a.index is None else a.index) == (cur if b.index is None else b.index)
+
+
+def is_replay_view(batch):
+    """True for a SampledBatch that still reads its replay buffer's storage through episode ids."""
+    return isinstance(batch, SampledBatch) and not batch.dense
+
+
 class SampledBatch(EpisodeBatch):
-    """A sampled view of a ReplayBuffer: (storage, episode ids, t_len). Zero-copy; gathered on access."""
+    """A sampled view of a ReplayBuffer: (storage, episode ids, t_len). Zero-copy; gathered on access.
+    After `.to(<another device>)` it is a dense EpisodeBatch on that device (`dense` = True)."""
+
+    dense = False
 
     def __init__(self, source, ep_ids, t_len=None):
         self.source = source
@@ -198,6 +220,8 @@ class SampledBatch(EpisodeBatch):
                          preprocess=None, device=source.device)
 
     def __getitem__(self, item):
+        if self.dense:
+            return EpisodeBatch.__getitem__(self, item)
         if isinstance(item, tuple) and len(item) == 2 and isinstance(item[0], slice) and item[0] == slice(None) \
                 and isinstance(item[1], slice) and item[1].start in (None, 0) and item[1].step in (None, 1):
             stop = self.t_len if item[1].stop is None else min(int(item[1].stop), self.t_len)
@@ -238,7 +262,7 @@ class SampledBatch(EpisodeBatch):
 
     def max_t_filled(self):
         lens = self.source.episode_lengths
-        if lens is not None:
+        if lens is not None:   # host lengths: valid for the dense copy too (same episodes, same t_len)
             return int(min(lens[self.ep_ids_np].max(), self.t_len))
         return int(self.materialize().max_t_filled())
 
@@ -246,11 +270,31 @@ class SampledBatch(EpisodeBatch):
         """Contiguous slice [rank*B/world, (rank+1)*B/world) of the episodes (data-parallel learner)."""
         from ..learners.dp import shard_bounds
         lo, hi = shard_bounds(len(self.ep_ids_np), rank, world)
+        if self.dense:
+            return EpisodeBatch.__getitem__(self, slice(lo, hi))
         return SampledBatch(self.source, self.ep_ids_np[lo:hi], self.t_len)
 
     def to(self, device):
-        if th.device(device) != th.device(self.device):
-            raise ValueError("a SampledBatch lives with its replay buffer; move the ReplayBuffer instead")
+        """EpisodeBatch.to (episode_buffer.py:91-96), in place as run.py:214-215 calls it. On the buffer's own device
+        it is a no-op (the kernels gather by id from the buffer). Otherwise — a host-resident buffer
+        (buffer_cpu_only) moving to the GPU — the sampled episodes are gathered on the host, truncated to t_len
+        (the reference's fancy index + `[:, :max_t]`, :205-217), and each field is copied to `device` once, from
+        pinned memory on the current stream. The batch is dense from then on."""
+        if _same_device(device, self.device):
+            return self
+        mat = self.materialize()
+        to_gpu = th.device(device).type == "cuda"
+        moved = SN(transition_data={}, episode_data={})
+        for src, dst in ((mat.data.transition_data, moved.transition_data),
+                         (mat.data.episode_data, moved.episode_data)):
+            for k, v in src.items():
+                v = v.contiguous()
+                if to_gpu and v.device.type == "cpu":
+                    v = v.pin_memory()
+                dst[k] = v.to(device, non_blocking=to_gpu)
+        self.data = moved
+        self.device = device
+        self.dense = True
         return self
 
 

@@ -731,4 +731,16 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
   }
 }
 
+// After the chain: if its error word (cstate[3]) is set, put the critic params and square_avg back to the copy
+// taken before the launch (a timed-out chain leaves workgroups at different steps, with W1 tiles never written back).
+__global__ __launch_bounds__(256) void coma_chain_restore_kernel(const int* __restrict__ cstate,
+                                                                 const float* __restrict__ bak, float* __restrict__ P,
+                                                                 float* __restrict__ SQ, int64_t Pc) {
+  if (cstate[3] == 0) return;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < Pc; i += (int64_t)gridDim.x * 256) {
+    P[i] = bak[i];
+    SQ[i] = bak[Pc + i];
+  }
+}
+
 }  // namespace mq

@@ -17,6 +17,7 @@ struct mc_handle {
   // critic workspace
   float *X, *H1t, *H2t, *Qt, *tgt, *msum, *H1p, *H1c, *H2c, *dH1c, *dH2c, *dqc, *qvals, *cpart, *cnorm, *crec;
   float *Pshadow, *SQshadow;
+  float* Pbak;   // [2][Pc] critic params / square_avg before the chain: restored if a hand-off times out
   int* actc;
   int* cstate;
   // actor workspace
@@ -173,6 +174,7 @@ int mc_create(const mc_config* cfg, mc_handle** out) {
       ns2 * (A * mq::H + A),       // slab_fc2
       red_tmp,                     // red_tmp
       4096,                        // norm_part
+      2 * h->Pc,                   // Pbak
   };
   const int NS = (int)(sizeof(sizes) / sizeof(sizes[0]));
   int64_t total = 0, offs[32];
@@ -194,6 +196,7 @@ int mc_create(const mc_config* cfg, mc_handle** out) {
   h->cstate = (int*)(b + offs[k++]);
   h->dL = b + offs[k++]; h->dHo = b + offs[k++]; h->pi = b + offs[k++]; h->ppart = b + offs[k++];
   h->slab_fc2 = b + offs[k++]; h->red_tmp = b + offs[k++]; h->norm_part = b + offs[k++];
+  h->Pbak = b + offs[k++];
   const char* ev = std::getenv("MQ_COMA_CHAIN");
   h->chain_env = !(ev && ev[0] == '0');
   int dev = 0;
@@ -375,11 +378,20 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
       MQ_HIP(hipFuncSetAttribute((const void*)coma_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       h->chain_attr = true;
     }
+    // the chain updates the critic in place: keep the pre-train version, restored below if a hand-off times out
+    MQ_HIP(hipMemcpyAsync(h->Pbak, h->critic, (size_t)h->Pc * sizeof(float), hipMemcpyDeviceToDevice, s));
+    MQ_HIP(hipMemcpyAsync(h->Pbak + h->Pc, h->csq, (size_t)h->Pc * sizeof(float), hipMemcpyDeviceToDevice, s));
     void* args[] = {&cc};
     const hipError_t e = hipLaunchCooperativeKernel((const void*)coma_chain_kernel, dim3(cc.NG), dim3(CC_THREADS),
                                                     args, (unsigned)lds, s);
     if (e == hipSuccess) {
       chained = true;
+      // failure semantics: after a timed-out hand-off the critic (params, square_avg) is put back to its pre-train
+      // version here and the actor's apply is skipped (its halt word), so the learner state is this train()'s
+      // starting state and COMALearner.train raises
+      hipLaunchKernelGGL(coma_chain_restore_kernel, dim3(64), dim3(256), 0, s, (const int*)h->cstate,
+                         (const float*)h->Pbak, h->critic, h->csq, h->Pc);
+      MQ_HIP(hipGetLastError());
       if (h->chain_trace) {   // debug: per-phase spans of workgroup 0 (100 MHz clock), averaged over <= 16 steps
         unsigned long long hb[16 * 8];
         MQ_HIP(hipMemcpyAsync(hb, h->chain_trace, sizeof(hb), hipMemcpyDeviceToHost, s));
@@ -394,7 +406,12 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
       (void)hipGetLastError();
       h->chain_env = false;
     }
-    if (chained && try_overlap) {   // launched after the chain, so the chain's workgroups are dispatched first
+    // Launched after the chain on a low-priority stream, so the chain's workgroups are normally dispatched first.
+    // That order is a heuristic across hardware queues, not a guarantee: if actor workgroups take CUs first, the
+    // chain's late workgroups start when they finish (the actor never waits on the chain), well inside the chain's
+    // spin bound (CC_SPIN_LIMIT polls, orders of magnitude longer than the actor unroll); a timeout would still be
+    // loud and leave the learner state unchanged (restore above)
+    if (chained && try_overlap) {
       MQ_HIP(hipStreamWaitEvent(ah->side, ah->ev_fork, 0));
       if ((rc = agent_forward(ah->side)) != MQ_OK) return rc;
       MQ_HIP(hipEventRecord(ah->ev_join, ah->side));
@@ -504,7 +521,8 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
     OptHP hp{c.lr, c.optim_alpha, c.optim_eps, c.grad_norm_clip, 1};
     const int blocks = (int)std::min<int64_t>((h->Pa + 255) / 256, 1024);
     hipLaunchKernelGGL(apply_kernel, dim3(blocks), dim3(256), 0, s, h->agent, h->agrad, h->asq, h->Pa,
-                       (const float*)h->norm_part, nnorm, hp, h->stats + 8);
+                       (const float*)h->norm_part, nnorm, hp, h->stats + 8,
+                       chained ? (const int*)(h->cstate + 3) : (const int*)nullptr);   // no actor step after a failure
     MQ_HIP(hipGetLastError());
   }
   hipLaunchKernelGGL(coma_stats_kernel, dim3(1), dim3(64), 0, s, (const float*)h->crec, T,

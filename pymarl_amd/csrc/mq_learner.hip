@@ -236,15 +236,16 @@ struct RedBuilder {
   int b1 = 0, b2 = 0;
   float* tmp;
   explicit RedBuilder(float* t) : tmp(t) {}
-  void add(const float* src, int nslab, int64_t len, float* dst, bool sq, int64_t pitch = 0, bool direct_ok = false) {
-    if (len <= 0 || nslab <= 0) return;
+  // returns true when the region is summed by pass 2 straight from its slabs (no pass-1 blocks read them)
+  bool add(const float* src, int nslab, int64_t len, float* dst, bool sq, int64_t pitch = 0, bool direct_ok = false) {
+    if (len <= 0 || nslab <= 0) return false;
     RedRegion& R = pl.r[pl.nr++];
     R.src = src; R.dst = dst; R.len = len; R.pitch = pitch > 0 ? pitch : len; R.nslab = nslab; R.sq = sq ? 1 : 0;
     if (direct_ok && nslab <= kRedZ) {   // pass 2 sums the slabs themselves: no pass-1 blocks, no tmp
       R.zc = 1; R.ng = nslab; R.tmp = (float*)src; R.tpitch = R.pitch; R.vec = 0; R.xcd = 0;
       R.blk1 = b1;
       R.blk2 = b2; b2 += (int)((len + 255) / 256);
-      return;
+      return true;
     }
     R.tpitch = len;
     // at most kRedZ groups, so pass 2 sums <= 16 partials per element with all loads in flight
@@ -258,6 +259,7 @@ struct RedBuilder {
     const int nb = (int)((len + 255) / 256), nb1 = R.vec ? (int)((len + 1023) / 1024) : nb;
     R.blk1 = b1; b1 += nb1 * R.ng;
     R.blk2 = b2; b2 += nb;
+    return false;
   }
 };
 
@@ -577,7 +579,8 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
     if (dwh_fused) {
       tj = (d.NH + DWH_T - 1) / DWH_T;
       ts = (d.S + 1 + DWH_T - 1) / DWH_T;
-      ns = std::max(1, std::min({h->dwh_split, kNsplitMax, (d.M + 1) / 2}));
+      // pass 1 shares this launch with dW_hyper, so dW_hyper's slabs must go straight to pass 2: at most kRedZ
+      ns = std::max(1, std::min({h->dwh_split, kRedZ, (d.M + 1) / 2}));
       h->nsplit_mix = ns;
       ndwh = tj * ts * ns;
     }
@@ -586,7 +589,9 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
     rb.add(w.slab_rnn, h->nblk_bwd, h->len_rnn, h->grad + h->off[MQ_P_RNN_W_IH], true);
     if (c.mixer == MQ_MIXER_QMIX) {
       // dW_hyper's few m-slice slabs go straight to pass 2 (they are written in the same launch as pass 1)
-      rb.add(w.slab_mix, h->nsplit_mix, h->len_mix, h->grad + h->off[MQ_P_HW1_W], true, 0, true);
+      const bool direct = rb.add(w.slab_mix, h->nsplit_mix, h->len_mix, h->grad + h->off[MQ_P_HW1_W], true, 0, true);
+      if (dwh_fused && !direct)   // pass-1 blocks would read slabs the dW_hyper blocks of the same grid still write
+        return set_err(MQ_ERR_STATE, "dW_hyper fused with reduction pass 1 needs a direct slab region");
       rb.add(w.slab_v2, h->nblk_mix, d.E + 1, h->grad + h->off[MQ_P_V2_W], true);
     }
     rb.add(w.loss_part, h->nblk_mix, MQ_NSUMS, h->grad + h->P, false);
@@ -634,7 +639,7 @@ int mq_apply(mq_handle* h, void* stream) {
   OptHP hp{h->cfg.lr, h->cfg.optim_alpha, h->cfg.optim_eps, h->cfg.grad_norm_clip, h->cfg.n_agents};
   int blocks = (int)std::min<int64_t>((h->P + 255) / 256, 1024);
   hipLaunchKernelGGL(apply_kernel, dim3(blocks), dim3(256), 0, s, h->on, h->grad, h->sq, h->P,
-                     (const float*)h->w.norm_part, h->n_norm_part, hp, h->stats);
+                     (const float*)h->w.norm_part, h->n_norm_part, hp, h->stats, (const int*)nullptr);
   MQ_HIP(hipGetLastError());
   pt.end();
   ++h->tstep;

@@ -129,7 +129,11 @@ struct OptHP {
 // the norm from the same partials in the same order, so all blocks agree bitwise.
 __global__ __launch_bounds__(256) void apply_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ sq,
                                                     int64_t n, const float* __restrict__ part, int npart,
-                                                    OptHP hp, float* __restrict__ stats) {
+                                                    OptHP hp, float* __restrict__ stats,
+                                                    const int* __restrict__ halt) {
+  // halt (may be NULL): a non-zero word means an earlier kernel of the step failed (the COMA critic chain's error
+  // word); the parameters, gradient and square_avg are then left untouched
+  if (halt && *halt != 0) return;
   __shared__ float sh[2];
   // the first element's operands and the mask sum do not depend on the norm: their loads go out before it
   const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x, stride = (int64_t)gridDim.x * 256;

@@ -28,7 +28,7 @@ from .. import _lib
 from ..modules.critics.coma import COMACritic
 from ..modules.flat import pack, rebind
 from .q_learner import replay_view
-from ..components.episode_buffer import SampledBatch
+from ..components.episode_buffer import is_replay_view
 
 
 def make_coma_config(args, input_dim, max_batch, max_seq):
@@ -117,7 +117,7 @@ class COMALearner:
         self._handle = None
 
     def _get_handle(self, batch):
-        T = batch.max_seq_length if not isinstance(batch, SampledBatch) else batch.source.max_seq_length
+        T = batch.source.max_seq_length if is_replay_view(batch) else batch.max_seq_length
         need_b = max(batch.batch_size, getattr(self.args, "batch_size", 1))
         if self._handle is None or self._handle_key[0] < need_b or self._handle_key[1] < T:
             cfg = make_coma_config(self.args, self.mac.agent.input_dim, need_b, T)
@@ -167,8 +167,10 @@ class COMALearner:
         st = self._stats.tolist()   # the one synchronisation per train(): stats + critic step count
         steps = int(round(st[9]))
         if steps < 0:
-            raise _lib.MQError("COMA critic chain: a workgroup hand-off timed out; this train()'s critic update is "
-                               "invalid (MQ_COMA_CHAIN=0 selects the three-launch critic)")
+            # the library put the critic back to its pre-train version and skipped the actor update: the learner's
+            # state is this call's starting state (no step counted), so a retry or MQ_COMA_CHAIN=0 can follow
+            raise _lib.MQError("COMA critic chain: a workgroup hand-off timed out; this train() was rolled back "
+                               "(critic and agent unchanged; MQ_COMA_CHAIN=0 selects the three-launch critic)")
         self.critic_training_steps += steps
         self._steps += 1
         for p in self.agent_params:

@@ -22,7 +22,7 @@ import torch as th
 from torch.optim import RMSprop
 
 from .. import _lib
-from ..components.episode_buffer import SampledBatch
+from ..components.episode_buffer import is_replay_view
 from ..modules.flat import pack, rebind
 from .dp import allreduce_grad_buffer
 from ..modules.mixers.qmix import QMixer
@@ -77,7 +77,7 @@ def replay_view(batch):
     Returns (struct, keepalive) — keep the second alive until the kernels that read it have been queued."""
     keep = []
     rep = _lib.MQReplay()
-    if isinstance(batch, SampledBatch):
+    if is_replay_view(batch):
         src = batch.source.data.transition_data
         tstride = batch.source.max_seq_length
         if len(batch.ep_ids_np) <= _lib.INLINE_IDS:
@@ -195,7 +195,7 @@ class QLearner:
         return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
     def _get_handle(self, batch):
-        T = batch.max_seq_length if not isinstance(batch, SampledBatch) else batch.source.max_seq_length
+        T = batch.source.max_seq_length if is_replay_view(batch) else batch.max_seq_length
         need_b = max(batch.batch_size, getattr(self.args, "batch_size", 1))
         key = (need_b, T)
         if self._handle is None or self._handle_key[0] < need_b or self._handle_key[1] < T:

@@ -22,5 +22,8 @@ class EpisodeRunner(BatchRollout):
                                  preprocess=preprocess, device=self.args.device)
         self.mac = mac
 
+    def n_test_episodes(self):
+        return self.args.test_nepisode   # episode_runner.py:105 compares with test_nepisode exactly
+
     def save_replay(self):
         self.env.save_replay()

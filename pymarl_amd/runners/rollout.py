@@ -38,6 +38,12 @@ class BatchRollout:
         self.train_stats, self.test_stats = {}, {}
         self.log_train_stats_t = self.log_train_stats_t0
 
+    def n_test_episodes(self):
+        """Test returns collected before the test stats are logged: the reference ParallelRunner rounds
+        test_nepisode to whole runs (parallel_runner.py:194-195); EpisodeRunner overrides it with test_nepisode
+        itself (episode_runner.py:105)."""
+        return max(1, self.args.test_nepisode // self.batch_size) * self.batch_size
+
     def get_env_info(self):
         return self.env_info
 
@@ -104,8 +110,7 @@ class BatchRollout:
         stats["n_episodes"] = stats.get("n_episodes", 0) + self.batch_size
         stats["ep_length"] = stats.get("ep_length", 0) + sum(lengths)
         rets.extend(returns)
-        n_test = max(1, self.args.test_nepisode // self.batch_size) * self.batch_size
-        if test_mode and len(self.test_returns) == n_test:
+        if test_mode and len(self.test_returns) == self.n_test_episodes():
             self._log(rets, stats, prefix)
         elif self.t_env - self.log_train_stats_t >= self.args.runner_log_interval:
             self._log(rets, stats, prefix)

@@ -63,11 +63,12 @@ class _Logger:
         self.stats.setdefault(key, []).append(float(value))
 
 
-def make_args(n, A, O, S, mixer, H=64, E=32):
+def make_args(n, A, O, S, mixer, H=64, E=32, double_q=True, obs_last_action=True, obs_agent_id=True):
     return SN(n_agents=n, n_actions=A, state_shape=S, obs_shape=O, rnn_hidden_dim=H, mixing_embed_dim=E,
               mixer=mixer, lr=5e-4, optim_alpha=0.99, optim_eps=1e-5, grad_norm_clip=10.0, gamma=0.99,
-              double_q=True, target_update_interval=200, learner_log_interval=0,
-              obs_last_action=True, obs_agent_id=True, agent="rnn", mac="basic_mac", agent_output_type="q",
+              double_q=double_q, target_update_interval=200, learner_log_interval=0,
+              obs_last_action=obs_last_action, obs_agent_id=obs_agent_id, agent="rnn", mac="basic_mac",
+              agent_output_type="q",
               action_selector="epsilon_greedy", epsilon_start=1.0, epsilon_finish=0.05, epsilon_anneal_time=50000,
               action_input_representation=None, obs_decoder=None, avail_actions_encoder=None,
               device="cpu", use_cuda=False)
@@ -86,7 +87,8 @@ def make_scheme(n, A, O, S):
 
 def build(case):
     n, A, O, S, T = case["n"], case["A"], case["O"], case["S"], case["T"]
-    args = make_args(n, A, O, S, case["mixer"])
+    flags = {k: case[k] for k in ("double_q", "obs_last_action", "obs_agent_id") if k in case}
+    args = make_args(n, A, O, S, case["mixer"], **flags)
     scheme = make_scheme(n, A, O, S)
     groups = {"agents": n}
     preprocess = {"actions": ("actions_onehot", [OneHot(out_dim=A)])}
@@ -100,7 +102,7 @@ def build(case):
     mac = BasicMAC(buf.scheme, groups, args)
     logger = _Logger()
     learner = QLearner(mac, buf.scheme, logger, args)
-    I = O + A + n
+    I = O + (A if args.obs_last_action else 0) + (n if args.obs_agent_id else 0)   # basic_controller.py:150-153
     w_agent = init_params(agent_param_shapes(I, 64, A), seed=case["weight_seed"])
     mac.agent.load_state_dict({k: th.from_numpy(v) for k, v in w_agent.items()})
     learner.target_mac.agent.load_state_dict({k: th.from_numpy(v) for k, v in w_agent.items()})
@@ -133,12 +135,17 @@ def intermediates(learner, batch):
         tmo.append(learner.target_mac.forward(batch, t=t))
     tmo = th.stack(tmo[1:], dim=1)
     tmo[avail_actions[:, 1:] == 0] = -9999999
-    mod = mac_out.clone().detach()
-    mod[avail_actions == 0] = -9999999
-    cur_max = mod[:, 1:].max(dim=3, keepdim=True)[1]
-    top2 = th.topk(mod[:, 1:], 2, dim=3)[0]
+    if args.double_q:   # q_learner.py:71-76
+        mod = mac_out.clone().detach()
+        mod[avail_actions == 0] = -9999999
+        cur_max = mod[:, 1:].max(dim=3, keepdim=True)[1]
+        top2 = th.topk(mod[:, 1:], 2, dim=3)[0]
+        target_max = th.gather(tmo, 3, cur_max).squeeze(3)
+    else:               # q_learner.py:77-78; the argmax and margin recorded are the target net's
+        cur_max = tmo.max(dim=3, keepdim=True)[1]
+        top2 = th.topk(tmo, 2, dim=3)[0]
+        target_max = tmo.max(dim=3)[0]
     margin = (top2[..., 0] - top2[..., 1])
-    target_max = th.gather(tmo, 3, cur_max).squeeze(3)
     if learner.mixer is not None:
         q_tot = learner.mixer(chosen, batch["state"][:, :-1])
         tq_tot = learner.target_mixer(target_max, batch["state"][:, 1:])
@@ -234,8 +241,12 @@ def run_case(name, case):
     for key in ["loss", "grad_norm", "td_error_abs", "q_taken_mean", "target_mean"]:
         out["stat_" + key] = np.array(logger.stats[key], dtype=np.float64)
     if cur_max_steps:
-        out["cur_max_actions"] = np.stack(cur_max_steps)
-        out["margin"] = np.stack(margin_steps)
+        # ragged batches truncate to different max_t: pad the time axis to T (padded slots: action 0, margin -1, so
+        # no test counts them as a clear decision; readers slice [:, :max_t - 1])
+        Tm = max(a.shape[1] for a in cur_max_steps)
+        pad = lambda a, v: np.pad(a, ((0, 0), (0, Tm - a.shape[1]), (0, 0)), constant_values=v)  # noqa: E731
+        out["cur_max_actions"] = np.stack([pad(a, 0) for a in cur_max_steps])
+        out["margin"] = np.stack([pad(m, -1.0) for m in margin_steps])
     if full:
         out["step_params"] = np.stack(per_step["params"])
         out["targets_final"] = per_step["targets"][-1]
@@ -259,6 +270,10 @@ CFG3 = dict(n=27, A=36, O=285, S=1170, T=180, B=4, n_episodes=8, data_seed=0, we
             ragged=True, steps=4, episodes=[0, 8, 200, 208], full=False, record_actions_steps=2)
 CFG4 = dict(n=5, A=11, O=80, S=120, T=120, B=64, n_episodes=96, data_seed=0, weight_seed=1, sampler_seed=2,
             ragged=False, steps=4, episodes=[0, 8, 200, 208], full=False, record_actions_steps=2)
+
+CFG1 = dict(n=3, A=9, O=30, S=48, T=60, B=8, n_episodes=40, data_seed=6, weight_seed=7, sampler_seed=8,
+            ragged=True, steps=10, episodes=[8 * k for k in range(5)] + [200 + 8 * k for k in range(5)],
+            full=False, record_actions_steps=10)
 
 # Batches past the fused kernels' row limits (R = B * n rows): R in (512, 1024] runs gru_fwd_kernel<2>, (1024, 2048]
 # gru_fwd_kernel<4>, > 2048 gru_fwd_kernel<8>; B > 256 (MQ_INLINE_IDS) passes the episode ids as a device vector.
@@ -289,6 +304,17 @@ CASES = {
     "cfg3_qmix": dict(CFG3, mixer="qmix", steps=3, episodes=[0, 8, 200], store_params=False),
     # BASELINE configs[3] shape (2s3z, QMIX): one rank's shard of B=512 over 8 GPUs, R = 64*5 = 320 rows > 256
     "cfg4_qmix": dict(CFG4, mixer="qmix"),
+    # the reference branches no shipped config takes: double_q: False (q_learner.py:77-78), obs_last_action /
+    # obs_agent_id: False (basic_controller.py:111-120, 150-153)
+    "tiny_qmix_nodq": dict(TINY, mixer="qmix", double_q=False),
+    "tiny_qmix_nola": dict(TINY, mixer="qmix", obs_last_action=False),
+    "tiny_vdn_noid": dict(TINY, mixer="vdn", obs_agent_id=False),
+    "tiny_qmix_bare": dict(TINY, mixer="qmix", obs_last_action=False, obs_agent_id=False, double_q=False),
+    "cfg2_qmix_nodq": dict(CFG2, mixer="qmix", double_q=False, steps=5, episodes=[0, 8, 200, 208, 216]),
+    # BASELINE configs[0]'s learner shape (QMIX on SMAC 3m, batch_size 8, upstream-SMAC obs / state: SURVEY §8a
+    # cfg1): n = 3, A = 9, O = 30, S = 48, T = 60, B = 8; ragged like SMAC episodes, a target update at step 5
+    "cfg1_qmix": dict(CFG1, mixer="qmix"),
+    "cfg1_vdn": dict(CFG1, mixer="vdn", steps=5, episodes=[0, 8, 200, 208, 216]),
 }
 
 if __name__ == "__main__":

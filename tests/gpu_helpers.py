@@ -20,8 +20,9 @@ CKPT = {name: "ckpt_{}_step2".format(name) for name in ("tiny_qmix", "tiny_vdn")
 def make_args(case, **over):
     a = SN(n_agents=case.n, n_actions=case.A, state_shape=case.S, obs_shape=case.O, rnn_hidden_dim=64,
            mixing_embed_dim=32, mixer=None if case.mixer == "none" else case.mixer, lr=5e-4, optim_alpha=0.99,
-           optim_eps=1e-5, grad_norm_clip=10.0, gamma=0.99, double_q=True, target_update_interval=200,
-           learner_log_interval=0, obs_last_action=True, obs_agent_id=True, agent="rnn", mac="basic_mac",
+           optim_eps=1e-5, grad_norm_clip=10.0, gamma=0.99, double_q=case.double_q, target_update_interval=200,
+           learner_log_interval=0, obs_last_action=case.obs_last_action, obs_agent_id=case.obs_agent_id,
+           agent="rnn", mac="basic_mac",
            agent_output_type="q", action_selector="epsilon_greedy", epsilon_start=1.0, epsilon_finish=0.05,
            epsilon_anneal_time=50000, batch_size=case.B, learner="q_learner", device="cuda", use_cuda=True)
     for k, v in over.items():
@@ -40,11 +41,14 @@ def make_scheme(case):
     }
 
 
-def build(case, device="cuda", **over):
+def build(case, device="cuda", buffer_device=None, **over):
+    """buffer_device: where the ReplayBuffer lives (default: with the learner); "cpu" is the reference's
+    buffer_cpu_only layout (run.py:137-139)."""
     args = make_args(case, **over)
     groups = {"agents": case.n}
     preprocess = {"actions": ("actions_onehot", [OneHot(out_dim=case.A)])}
-    buf = ReplayBuffer(make_scheme(case), groups, case.n_episodes, case.T + 1, preprocess=preprocess, device=device)
+    buf = ReplayBuffer(make_scheme(case), groups, case.n_episodes, case.T + 1, preprocess=preprocess,
+                       device=buffer_device or device)
     buf.load_arrays(case.data)
     mac = mac_REGISTRY["basic_mac"](buf.scheme, groups, args)
     logger = Logger(logging.getLogger("mq-test"))

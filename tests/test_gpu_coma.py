@@ -226,8 +226,10 @@ def test_coma_skipped_critic_steps(path, env, monkeypatch):
 
 def test_coma_chain_failure_is_loud(monkeypatch):
     """A persistent-chain workgroup that stops flagging (MQ_COMA_CHAIN_FAULT test hook) makes every workgroup leave
-    within the bounded spin: the launch ends, the stats come out NaN with critic_steps = -1 and train() raises;
-    the next train() runs normally."""
+    within the bounded spin: the launch ends, the stats come out NaN with critic_steps = -1 and train() raises.
+    The failed train() is rolled back: critic params / square_avg are restored and the actor update is skipped, so
+    every parameter and optimiser buffer is bitwise its pre-train value, and the next train() equals a clean
+    learner's first train() on the same batch bit for bit."""
     from tests.gpu_helpers import build_coma
     from pymarl_amd._lib import MQError
     monkeypatch.delenv("MQ_COMA_CHAIN", raising=False)
@@ -237,15 +239,26 @@ def test_coma_chain_failure_is_loud(monkeypatch):
     batch = buf.sample(c.B)
     batch = batch[:, :batch.max_t_filled()]
     mac.action_selector.epsilon = c.epsilon[0]
+    snap = lambda l: [t.cpu().numpy().copy() for t in (l._critic, l._csq, l._agent, l._asq, l._tcritic)]  # noqa
+    before = snap(learner)
     monkeypatch.setenv("MQ_COMA_CHAIN_FAULT", "1")
     with pytest.raises(MQError):
         learner.train(batch, 1000, 0)
     assert learner.critic_path() == "chain"
     assert np.isnan(learner._stats[0].item())
+    for a, b in zip(before, snap(learner)):
+        assert np.array_equal(a, b)
+    assert learner.critic_training_steps == 0
     monkeypatch.delenv("MQ_COMA_CHAIN_FAULT")
     learner.train(batch, 2000, 8)
     st = learner.last_stats()
     assert st["critic_steps"] > 0 and np.isfinite(st["critic_loss"])
+    _, _, mac2, clean, _ = build_coma(c)
+    mac2.action_selector.epsilon = c.epsilon[0]
+    clean.train(batch, 2000, 8)
+    for a, b in zip(snap(learner), snap(clean)):
+        assert np.array_equal(a, b)
+    assert learner.last_stats() == clean.last_stats()
 
 
 def test_coma_chain_bitwise_deterministic(coma_cases, monkeypatch):

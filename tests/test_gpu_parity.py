@@ -51,9 +51,13 @@ def classify_decisions(learner, o, nb, fw):
     """Compare the GPU's double-Q argmax and fc1 relu decisions with the oracle's at the same state.
     Returns (record, dq_flip_mask_ok, relu_flip_ok): the counts of decisions, near-ties and flips."""
     from oracle.qlearner_np import fc1_preacts
-    q = fw["mac_out"].copy()
-    q[nb["avail_actions"] == 0] = -9999999.0
-    top2 = -np.sort(-q[:, 1:], axis=3)[..., :2]
+    if o.cfg.get("double_q", True):   # the online net's masked argmax (q_learner.py:71-76)
+        q = fw["mac_out"].copy()
+        q[nb["avail_actions"] == 0] = -9999999.0
+        q = q[:, 1:]
+    else:                             # target_mac_out.max(dim=3) (q_learner.py:77-78), masked at :68
+        q = fw["target_mac_out"]
+    top2 = -np.sort(-q, axis=3)[..., :2]
     margin = top2[..., 0] - top2[..., 1]
     tie = margin <= MARGIN_EPS * np.maximum(1.0, np.abs(top2[..., 0]))
     # live transitions (q_learner.py:39-44 mask): padded slots (every action masked) are ties by construction but
@@ -62,7 +66,7 @@ def classify_decisions(learner, o, nb, fw):
     got = learner.last_cur_max_actions().cpu().numpy()
     dq_flip = got != fw["cur_max_actions"]
     on_gpu = learner.last_intermediate(3).cpu().numpy() > 0
-    pre = fc1_preacts(o.p, nb["obs"], nb["actions_onehot"])
+    pre = fc1_preacts(o.p, nb["obs"], nb["actions_onehot"], o.input_flags)
     relu_tie = np.abs(pre) <= RELU_EPS
     relu_flip = on_gpu != (pre > 0)
     rec = dict(dq_decisions=int(live.sum()), dq_ties=int((tie & live).sum()), dq_masked_slots=int((~live).sum()),
@@ -141,10 +145,12 @@ def run_case(case, check_full, plan=None):
             r["rel_err_" + s_] = abs(st[s_] - ref) / max(abs(ref), 1e-12)
             r["shadow_rel_err_" + s_] = abs(st[s_] - st2[s_]) / max(abs(st2[s_]), 1e-12)
         if "cur_max_actions" in case.z and k < case.z["cur_max_actions"].shape[0]:
-            ref = case.z["cur_max_actions"][k].astype(np.int64)
-            mo = learner.last_intermediate(0).cpu().numpy()[:, 1:max_t]
+            Tk = got.shape[1]   # ragged fixtures pad the time axis
+            ref = case.z["cur_max_actions"][k][:, :Tk].astype(np.int64)
+            # the decision's own Q: the online net under double-Q, else the target net (q_learner.py:71-78)
+            mo = learner.last_intermediate(0 if case.double_q else 1).cpu().numpy()[:, 1:max_t]
             mo = np.where(nb["avail_actions"][:, 1:] == 0, np.float32(-9999999.0), mo)
-            clear = case.z["margin"][k] > MARGIN_EPS * np.maximum(1.0, np.abs(mo.max(axis=3)))
+            clear = case.z["margin"][k][:, :Tk] > MARGIN_EPS * np.maximum(1.0, np.abs(mo.max(axis=3)))
             r["ref_dq_mismatch_clear"] = int((got != ref)[clear].sum())
             r["ref_dq_mismatch_ties"] = int((got != ref)[~clear].sum())
         rec.append(r)
@@ -195,13 +201,14 @@ def run_case(case, check_full, plan=None):
     return learner
 
 
-@pytest.mark.parametrize("name", ["tiny_qmix_full", "tiny_qmix", "tiny_vdn", "tiny_iql"])
+@pytest.mark.parametrize("name", ["tiny_qmix_full", "tiny_qmix", "tiny_vdn", "tiny_iql", "tiny_qmix_nodq",
+                                  "tiny_qmix_nola", "tiny_vdn_noid", "tiny_qmix_bare"])
 def test_tiny_full(cases, name):
     run_case(get_case(cases, name), check_full=True)
 
 
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_vdn", "cfg2_qmix_ragged", "cfg2_iql", "cfg3_vdn", "cfg3_qmix",
-                                  "cfg4_qmix"])
+                                  "cfg4_qmix", "cfg2_qmix_nodq", "cfg1_qmix", "cfg1_vdn"])
 def test_cfg2_trajectory(cases, name):
     run_case(get_case(cases, name), check_full=False)
 
@@ -299,12 +306,44 @@ UNFUSED_ENV = ("MQ_UNFUSED_FWD", "MQ_UNFUSED_BWD", "MQ_GEMM_HYPER")
     ("tiny_iql", 4, False), ("cfg2_iql", 4, False), ("rw2_qmix", 3, False), ("rw4_vdn", 3, False),
     ("wide_qmix", 3, False), ("cfg3_vdn_b128", 2, False),
     # the A/B switches: the unfused kernel sequence on the shapes the fused kernels normally take
-    ("cfg2_qmix", 4, True), ("cfg2_qmix_ragged", 3, True), ("tiny_vdn", 2, True)])
+    ("cfg2_qmix", 4, True), ("cfg2_qmix_ragged", 3, True), ("tiny_vdn", 2, True), ("tiny_qmix_bare", 2, True),
+    # reference branches no shipped config takes (double_q / obs_last_action / obs_agent_id = False) and BASELINE
+    # configs[0]'s learner shape (3m: n = 3, A = 9, O = 30, S = 48, T = 60, B = 8)
+    ("tiny_qmix_nodq", 4, False), ("tiny_qmix_nola", 4, False), ("tiny_vdn_noid", 4, False),
+    ("tiny_qmix_bare", 4, False), ("cfg2_qmix_nodq", 5, False), ("cfg1_qmix", 10, False), ("cfg1_vdn", 5, False)])
 def test_teacher_forced_steps(cases, name, steps, unfused, monkeypatch):
     run_teacher_forced(get_case(cases, name), steps, unfused, monkeypatch)
 
 
-def run_teacher_forced(case, steps, unfused, monkeypatch):
+@pytest.mark.parametrize("name,steps,flow", [
+    ("tiny_qmix", 4, "cpu_to"), ("cfg2_qmix", 3, "cpu_to"), ("cfg2_qmix_ragged", 3, "cpu_to"), ("cfg1_qmix", 4, "cpu_to"),
+    ("tiny_vdn", 3, "cpu_to"), ("tiny_qmix", 4, "dense_slice"), ("cfg2_qmix_ragged", 3, "dense_slice")])
+def test_reference_replay_flows(cases, name, steps, flow, monkeypatch):
+    """The learner fed the way the reference's run loop feeds it, teacher-forced against the oracle with step 0 also
+    against the reference's own golden stats:
+    * cpu_to: buffer_cpu_only (run.py:137-139) — a host ReplayBuffer, then sample -> max_t_filled -> [:, :max_t] ->
+      `.to(args.device)` in place (run.py:208-215) -> train; the moved batch is dense (no episode ids) and the
+      learner takes the dense kernel path;
+    * dense_slice: a dense device EpisodeBatch of the full T + 1 steps sliced to [:, :max_t] (the reference's own
+      buffer kept on the GPU), so the kernels read it with t_stride = T + 1 > t_len."""
+    run_teacher_forced(get_case(cases, name), steps, False, monkeypatch, flow=flow)
+
+
+def sample_like_reference(buf, case, args, flow):
+    """One batch as run.py:207-215 builds it (flow "view": this repo's HBM replay view, ids gathered in-kernel)."""
+    batch = buf.sample(case.B)
+    if flow == "dense_slice":
+        full = batch.materialize()   # a dense [B][T+1] device EpisodeBatch, as the reference's __getitem__ returns
+        return full[:, :batch.max_t_filled()]
+    max_ep_t = batch.max_t_filled()
+    batch = batch[:, :max_ep_t]
+    if flow == "cpu_to" and batch.device != args.device:
+        batch.to(args.device)
+        assert batch.dense and batch["obs"].is_cuda
+    return batch
+
+
+def run_teacher_forced(case, steps, unfused, monkeypatch, flow="view"):
     """Every step from the oracle's state; decisions, stats, gradients and the RMSprop step checked (see module doc)."""
     from oracle.qlearner_np import OracleQLearner
     from tests.gpu_helpers import build, flat_grads, flat_params, rel
@@ -314,19 +353,27 @@ def run_teacher_forced(case, steps, unfused, monkeypatch):
             monkeypatch.setenv(k, "1")
         else:
             monkeypatch.delenv(k, raising=False)
-    args, buf, mac, learner, logger = build(case)
+    args, buf, mac, learner, logger = build(case, buffer_device="cpu" if flow == "cpu_to" else None)
     o = OracleQLearner(case.agent_params, case.mixer_params, case.cfg())
     np.random.seed(case.sampler_seed)
     rec = []
+    strided = 0
     for k in range(steps):
-        batch = buf.sample(case.B)
-        batch = batch[:, :batch.max_t_filled()]
+        batch = sample_like_reference(buf, case, args, flow)
+        if flow == "dense_slice":
+            strided += int(batch["obs"].stride(0) != batch.max_seq_length * case.n * case.O)
         nb, _ = case.batch(k)
         set_state_from_oracle(learner, o)
         p_prev, sq_prev = o.flat("params").astype(np.float64), o.flat("sq").astype(np.float64)
         fw = o.forward(nb)
         learner.train(batch, 1000 * k, case.episodes[k])
         st = learner.last_stats()
+        if flow != "view":
+            assert learner.last_plan()["inline_ids"] == 0, "a dense batch must not take the episode-id path"
+        if k == 0:   # the same starting state as the reference's golden run: its logged stats
+            for s_ in STATS:
+                ref = float(case.z["stat_" + s_][0])
+                assert abs(st[s_] - ref) <= 1e-4 * abs(ref) + 1e-6, (name, flow, s_, st[s_], ref)
         r, got, on_gpu = classify_decisions(learner, o, nb, fw)
         r["step"] = k
         rec.append(r)
@@ -350,7 +397,9 @@ def run_teacher_forced(case, steps, unfused, monkeypatch):
         assert rel(learner._sq.cpu().numpy(), sq_exp) < 1e-5, (name, k)
         assert rel(flat_params(learner), p_exp) < 1e-6, (name, k)
         assert np.abs(flat_params(learner) - o.flat("params")).max() <= 20 * 5e-4, (name, k)
-    write_record("teacher" + ("_unfused" if unfused else ""), name, rec)
+    if flow == "dense_slice":
+        assert strided > 0, "no step ran with t_stride > t_len"
+    write_record("teacher" + ("_unfused" if unfused else "") + ("" if flow == "view" else "_" + flow), name, rec)
 
 
 def test_data_parallel_norm_path_single_rank(cases):
@@ -410,6 +459,29 @@ def test_dwh_fused_reduction_bitwise(cases, name, monkeypatch):
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.array_equal(outs[0][1], outs[1][1])
     assert outs[0][2] == outs[1][2]
+
+
+def test_dwh_split_clamped_when_fused(cases, monkeypatch):
+    """MQ_DWH_SPLIT above kRedZ = 16: the fused dW_hyper + reduction-pass-1 launch clamps its m-slices to 16 (its
+    slabs must go straight to pass 2, never read by pass-1 blocks of the same grid), so the result is bitwise the
+    split-16 run's, and both match the oracle teacher-forced."""
+    from tests.gpu_helpers import build, flat_grads, flat_params
+    case = get_case(cases, "cfg2_qmix")
+    monkeypatch.delenv("MQ_DWH_UNFUSED", raising=False)
+    outs = []
+    for split in ("32", "16"):
+        monkeypatch.setenv("MQ_DWH_SPLIT", split)
+        args, buf, mac, learner, logger = build(case)
+        np.random.seed(case.sampler_seed)
+        for k in range(2):
+            batch = buf.sample(case.B)
+            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
+        th.cuda.synchronize()
+        outs.append((flat_params(learner), flat_grads(learner), learner.last_stats()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
+    monkeypatch.setenv("MQ_DWH_SPLIT", "32")
+    run_teacher_forced(case, 2, False, monkeypatch)
 
 
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_qmix_ragged", "tiny_qmix"])

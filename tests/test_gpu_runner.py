@@ -13,10 +13,12 @@ import torch as th
 
 pytestmark = pytest.mark.gpu
 
-N, A, O, S, LIMIT = 3, 9, 30, 48, 24
+# BASELINE configs[0]'s shape (SMAC 3m, upstream obs / state sizes): episode_limit 60
+N, A, O, S, LIMIT = 3, 9, 30, 48, 60
+MARGIN_EPS = 1e-5   # argmax-equal wherever the top-2 gap exceeds 1e-5 * max(1, |Q|)
 
 
-def build(kind="episode", bsr=1):
+def build(kind="episode", bsr=1, cpu_only=False):
     from pymarl_amd.components.episode_buffer import ReplayBuffer
     from pymarl_amd.components.transforms import OneHot
     from pymarl_amd.controllers import REGISTRY as mac_REGISTRY
@@ -30,7 +32,8 @@ def build(kind="episode", bsr=1):
               epsilon_start=1.0, epsilon_finish=0.05, epsilon_anneal_time=500, batch_size=8, batch_size_run=bsr,
               env="fake", env_args=dict(n_agents=N, n_actions=A, obs_dim=O, state_dim=S, episode_limit=LIMIT, seed=4,
                                         end_threshold=None if kind == "episode" else -0.9),
-              device="cuda", use_cuda=True, test_nepisode=1, runner_log_interval=10 ** 9, learner="q_learner")
+              device="cuda", use_cuda=True, test_nepisode=1, runner_log_interval=10 ** 9, learner="q_learner",
+              buffer_cpu_only=cpu_only)
     logger = Logger(logging.getLogger("runner-test"))
     runner = r_REGISTRY[kind](args, logger)
     scheme = {"state": {"vshape": S}, "obs": {"vshape": O, "group": "agents"},
@@ -39,7 +42,8 @@ def build(kind="episode", bsr=1):
               "reward": {"vshape": (1,)}, "terminated": {"vshape": (1,), "dtype": th.uint8}}
     groups = {"agents": N}
     preprocess = {"actions": ("actions_onehot", [OneHot(out_dim=A)])}
-    buf = ReplayBuffer(scheme, groups, 64, LIMIT + 1, preprocess=preprocess, device="cuda")
+    # run.py:137-139: the replay lives on the host under buffer_cpu_only
+    buf = ReplayBuffer(scheme, groups, 64, LIMIT + 1, preprocess=preprocess, device="cpu" if cpu_only else "cuda")
     mac = mac_REGISTRY["basic_mac"](buf.scheme, groups, args)
     runner.setup(scheme=scheme, groups=groups, preprocess=preprocess, mac=mac)
     learner = le_REGISTRY["q_learner"](mac, buf.scheme, logger, args)
@@ -60,10 +64,13 @@ def check_contract(b, i=0):
     return L
 
 
-@pytest.mark.parametrize("kind,bsr", [("episode", 1), ("parallel", 4)])
-def test_runner_greedy_actions_and_training(kind, bsr):
+@pytest.mark.parametrize("kind,bsr,cpu_only", [("episode", 1, False), ("parallel", 4, False), ("parallel", 4, True)])
+def test_runner_greedy_actions_and_training(kind, bsr, cpu_only):
+    """cpu_only: the reference's buffer_cpu_only layout — the ParallelRunner writes a host batch
+    (parallel_runner.py:45), the MAC moves each step's rows to the device, the host replay is sampled, truncated and
+    moved with `.to(args.device)` before train (run.py:208-219)."""
     from oracle.qlearner_np import agent_unroll
-    args, runner, buf, mac, learner = build(kind, bsr)
+    args, runner, buf, mac, learner = build(kind, bsr, cpu_only)
     np.random.seed(0)
     th.manual_seed(0)
     try:
@@ -76,7 +83,9 @@ def test_runner_greedy_actions_and_training(kind, bsr):
         b = runner.run(test_mode=True)
     finally:
         runner.close_env()
+    assert b.device == ("cpu" if cpu_only else "cuda")
     p = {k: v.detach().cpu().numpy() for k, v in mac.agent.state_dict().items()}
+    decisions = ties = tie_flips = 0
     for i in range(bsr):
         L = check_contract(b, i)
         obs = b["obs"][i:i + 1, :L + 1].cpu().numpy()
@@ -86,12 +95,21 @@ def test_runner_greedy_actions_and_training(kind, bsr):
         qm = np.where(av == 0, -np.inf, q)
         greedy = qm.argmax(-1)
         top2 = -np.sort(-qm, -1)[..., :2]
-        clear = (top2[..., 0] - top2[..., 1]) > 1e-4
+        tie = (top2[..., 0] - top2[..., 1]) <= MARGIN_EPS * np.maximum(1.0, np.abs(top2[..., 0]))
         rec = b["actions"][i:i + 1, :L + 1, :, 0].cpu().numpy()
-        assert np.array_equal(rec[clear], greedy[clear])
-    # training on runner-made episodes
+        # every greedy decision equals the oracle's masked argmax except near-ties, which are counted
+        assert np.array_equal(rec[~tie], greedy[~tie])
+        decisions += int(tie.size)
+        ties += int(tie.sum())
+        tie_flips += int((rec != greedy)[tie].sum())
+    print("greedy decisions {} near-ties {} near-tie flips {}".format(decisions, ties, tie_flips))
+    assert ties <= max(2, decisions // 100), (decisions, ties)   # near-ties are rare: a sanity bound
+    # training on runner-made episodes, sampled the way run.py:207-219 does
     for k in range(3):
         s = buf.sample(8)
-        learner.train(s[:, :s.max_t_filled()], runner.t_env, 10 + k)
+        s = s[:, :s.max_t_filled()]
+        if s.device != args.device:
+            s.to(args.device)
+        learner.train(s, runner.t_env, 10 + k)
         st = learner.last_stats()
         assert all(np.isfinite(v) for v in st.values()), st

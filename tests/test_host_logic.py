@@ -188,3 +188,16 @@ def test_logger_interface():
     lg.print_recent_stats()
     assert lines[-1].startswith("Recent Stats | t_env:          6 | Episode:       12\n")
     assert "loss:" in lines[-1] and "4.0000" in lines[-1]
+
+
+def test_test_stat_threshold_matches_reference_runners():
+    """When the runners log test stats: the reference ParallelRunner rounds test_nepisode to whole runs of
+    batch_size_run (parallel_runner.py:194-195), EpisodeRunner compares with test_nepisode exactly (episode_runner.py:105)."""
+    from types import SimpleNamespace as SN
+    from pymarl_amd.runners.episode_runner import EpisodeRunner
+    from pymarl_amd.runners.parallel_runner import ParallelRunner
+    for cls, bs, n, want in [(ParallelRunner, 4, 6, 4), (ParallelRunner, 4, 2, 4), (ParallelRunner, 8, 16, 16),
+                             (EpisodeRunner, 1, 3, 3), (EpisodeRunner, 1, 0, 0)]:
+        r = cls.__new__(cls)
+        r.args, r.batch_size = SN(test_nepisode=n), bs
+        assert r.n_test_episodes() == want, (cls.__name__, bs, n)

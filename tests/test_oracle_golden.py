@@ -19,7 +19,8 @@ MARGIN_EPS = 1e-5
 TIGHT_STEPS = 12
 
 
-@pytest.mark.parametrize("name", ["tiny_qmix", "tiny_vdn", "tiny_qmix_full", "cfg2_qmix_ragged", "tiny_iql"])
+@pytest.mark.parametrize("name", ["tiny_qmix", "tiny_vdn", "tiny_qmix_full", "cfg2_qmix_ragged", "tiny_iql",
+                                  "tiny_qmix_nodq", "tiny_qmix_nola", "tiny_vdn_noid", "tiny_qmix_bare"])
 def test_intermediates_and_params(golden_cases, name):
     c = golden_cases[name]
     o = OracleQLearner(c.agent_params, c.mixer_params, c.cfg())
@@ -44,7 +45,7 @@ def test_intermediates_and_params(golden_cases, name):
 
 
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_vdn", "cfg3_vdn", "cfg3_qmix", "cfg4_qmix", "cfg2_iql", "rw2_qmix",
-                                  "rw4_vdn", "wide_qmix", "cfg3_vdn_b128"])
+                                  "rw4_vdn", "wide_qmix", "cfg3_vdn_b128", "cfg2_qmix_nodq", "cfg1_qmix", "cfg1_vdn"])
 def test_cfg2_trajectory(golden_cases, name):
     c = golden_cases[name]
     o = OracleQLearner(c.agent_params, c.mixer_params, c.cfg())
@@ -52,8 +53,9 @@ def test_cfg2_trajectory(golden_cases, name):
         b, _ = c.batch(k)
         if k < c.z["cur_max_actions"].shape[0]:
             fw = o.forward(b)
-            ref = c.z["cur_max_actions"][k]
-            clear = c.z["margin"][k] > MARGIN_EPS
+            Tk = fw["cur_max_actions"].shape[1]   # ragged fixtures pad the time axis
+            ref = c.z["cur_max_actions"][k][:, :Tk]
+            clear = c.z["margin"][k][:, :Tk] > MARGIN_EPS
             assert np.array_equal(fw["cur_max_actions"][clear], ref[clear].astype(np.int64))
         st = o.train(b, 1000 * k, c.episodes[k])
         tol = 1e-4 if k < TIGHT_STEPS else 1e-2
