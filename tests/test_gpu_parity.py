@@ -317,7 +317,7 @@ def test_teacher_forced_steps(cases, name, steps, unfused, monkeypatch):
 
 @pytest.mark.parametrize("name,steps,flow", [
     ("tiny_qmix", 4, "cpu_to"), ("cfg2_qmix", 3, "cpu_to"), ("cfg2_qmix_ragged", 3, "cpu_to"), ("cfg1_qmix", 4, "cpu_to"),
-    ("tiny_vdn", 3, "cpu_to"), ("tiny_qmix", 4, "dense_slice"), ("cfg2_qmix_ragged", 3, "dense_slice")])
+    ("tiny_vdn", 3, "cpu_to"), ("tiny_qmix", 4, "dense_slice"), ("cfg1_qmix", 4, "dense_slice")])
 def test_reference_replay_flows(cases, name, steps, flow, monkeypatch):
     """The learner fed the way the reference's run loop feeds it, teacher-forced against the oracle with step 0 also
     against the reference's own golden stats:
@@ -357,11 +357,12 @@ def run_teacher_forced(case, steps, unfused, monkeypatch, flow="view"):
     o = OracleQLearner(case.agent_params, case.mixer_params, case.cfg())
     np.random.seed(case.sampler_seed)
     rec = []
-    strided = 0
+    strided = truncated = 0
     for k in range(steps):
         batch = sample_like_reference(buf, case, args, flow)
         if flow == "dense_slice":
             strided += int(batch["obs"].stride(0) != batch.max_seq_length * case.n * case.O)
+            truncated += int(batch.max_seq_length < case.T + 1)
         nb, _ = case.batch(k)
         set_state_from_oracle(learner, o)
         p_prev, sq_prev = o.flat("params").astype(np.float64), o.flat("sq").astype(np.float64)
@@ -397,8 +398,9 @@ def run_teacher_forced(case, steps, unfused, monkeypatch, flow="view"):
         assert rel(learner._sq.cpu().numpy(), sq_exp) < 1e-5, (name, k)
         assert rel(flat_params(learner), p_exp) < 1e-6, (name, k)
         assert np.abs(flat_params(learner) - o.flat("params")).max() <= 20 * 5e-4, (name, k)
-    if flow == "dense_slice":
-        assert strided > 0, "no step ran with t_stride > t_len"
+    if flow == "dense_slice":   # every truncated batch is read in place with t_stride = T + 1 > t_len
+        assert strided == truncated, (strided, truncated)
+        assert case.name != "cfg1_qmix" or strided == steps
     write_record("teacher" + ("_unfused" if unfused else "") + ("" if flow == "view" else "_" + flow), name, rec)
 
 
