@@ -344,18 +344,24 @@ def init_distributed(expect_world=None):
     return world, rank, device
 
 
-def dist_info(world):
+def dist_info(world, learner=None, what="all_reduce(sum) of the fused [grads | sums] buffer"):
     import torch.distributed as dist
     if world > 1 and dist.is_initialized():
+        how = learner.collective() if learner is not None else None
+        where = ("in stream order inside libmq_learner (the library's RCCL communicator, id broadcast once)"
+                 if how == "rccl-native" else "torch.distributed on a communication stream")
         return {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()),
-                "collective": "all_reduce(sum) of the fused [grads | sums] buffer, comm stream"}
+                "collective": "{}, {}".format(what, where), "path": how}
     return {"world_size": 1, "backend": None, "collective": None}
 
 
 def coma_bench(a):
-    """cfg5: COMALearner.train. N > 1 is data parallel with weak scaling (B = 8 episodes per rank): the critic's T
-    dependent optimiser steps make every live critic step an exchange, so each train() issues T + 3 all-reduces
-    (include/mc_coma.h, mc_set_data_parallel; SURVEY.md §8e "COMA caveat")."""
+    """cfg5: COMALearner.train on coma_smac's batch of B = 8 episodes (MMM2 shape: 80 critic rows). N > 1 is strong
+    scaling of that batch: every rank passes the same global sample, runs the critic's T dependent optimiser steps
+    on all of it through the persistent chain (replicated: no per-step exchange), the actor on its B / N episodes,
+    and ONE all-reduce sums the agent gradient (COMALearner "replicated" mode, include/mc_coma.h
+    mc_set_actor_shard). The exchange mode (T + 3 all-reduces, SURVEY.md §8e "COMA caveat") is the fallback for
+    batches the chain does not take."""
     import torch as th
     import torch.distributed as dist
     world, rank, device = init_distributed(a.gpus)
@@ -368,10 +374,9 @@ def coma_bench(a):
             dist.barrier()
 
     def step(k):
-        gb = buf.sample(B * world)
-        b = gb.shard(rank, world) if world > 1 else gb
+        gb = buf.sample(B)   # the global sample: the learner trains this rank's share of it
         mac.action_selector.epsilon = mac.action_selector.schedule.eval(1000 * k)
-        learner.train(b[:, :b.max_t_filled()], 1000 * k, 8 * k)
+        learner.train(gb[:, :gb.max_t_filled()], 1000 * k, 8 * k)
 
     for k in range(max(1, a.warmup)):
         step(k)
@@ -399,19 +404,21 @@ def coma_bench(a):
     R = B * n
     step_flops = 2 * R * (2 * Kc * 128 + 3 * 128 * 128 + 2 * 128 * A)   # one critic step, fwd + bwd
     achieved = step_flops / (chain_ms * 1e-3 / T) / 1e12
-    value = B * T * n * world * a.steps / dt
+    value = B * T * n * a.steps / dt
     if rank != 0:
         dist.destroy_process_group()
         return
     cpu = None if (a.no_cpu_baseline or world > 1) else coma_cpu_baseline(a.config, data)
     line = {
         "metric": METRIC, "value": value, "unit": "samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
         "dtype": "fp32", "data": "synthetic (SURVEY.md §8d replay recipe, random-init weights)",
         "config": {"workload": desc, "learner": "coma_learner", "n_agents": n, "n_actions": A, "obs_dim": O,
-                   "state_dim": S, "episode_limit": T, "batch_per_gpu": B, "global_batch": B * world,
-                   "replay_episodes": buf.buffer_size, "parallelism": f"dp{world}"},
-        "dist": dist_info(world),
+                   "state_dim": S, "episode_limit": T, "batch_per_gpu": B / world, "global_batch": B,
+                   "replay_episodes": buf.buffer_size, "parallelism": f"dp{world}",
+                   "coma_dp_mode": learner.dp_mode(B)},
+        "dist": dist_info(world, learner, "critic replicated on the whole batch, actor sharded: all_reduce(sum) of "
+                                          "the agent [grads | sums] buffer once per train"),
         "roofline": {"bound": "mfma", "kernel": ("coma_chain_kernel (one cooperative launch, T critic steps)"
                                                  if learner.critic_path() == "chain"
                                                  else "critic step chain (l1 + head + wgrad, x T)"),
@@ -554,7 +561,7 @@ def main():
             "config": {"workload": desc, "mixer": mixer, "n_agents": n, "n_actions": A, "obs_dim": O,
                        "state_dim": S, "episode_limit": T, "batch_per_gpu": B, "global_batch": B * world,
                        "replay_episodes": buf.buffer_size, "parallelism": f"dp{world}"},
-            "dist": dist_info(world),
+            "dist": dist_info(world, learner),
             "roofline": roof,
             "hbm_roofline_whole_step": {"achieved_GBs": value * bytes_per_sample / 1e9, "peak_GBs": HBM_PEAK_GBS,
                                         "frac": value * bytes_per_sample / 1e9 / HBM_PEAK_GBS},

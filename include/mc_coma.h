@@ -93,9 +93,19 @@ typedef int (*mc_allreduce_fn)(float* buf, int64_t count, void* stream, void* ct
 /* The same exchange steps over a native RCCL communicator (id from mq_comm_unique_id, one process per GPU): no
  * host callback per critic step. Replaces any mc_set_data_parallel callback; scratch is library-owned. */
 int mc_comm_attach(mc_handle* h, const uint8_t* id, int32_t rank, int32_t world);
+/* The same over a communicator the caller owns (see mq_comm_use): borrowed, never freed by the handle. */
+int mc_comm_use(mc_handle* h, void* nccl_comm);
 int mc_set_data_parallel(mc_handle* h, mc_allreduce_fn allreduce, void* ctx, int32_t rank, float* scratch,
                          int64_t scratch_count);
-/* 0 = critic Q values the actor used [T][B*n][A]; 1 = TD(lambda) targets [T][B*n]; 2 = policy pi [T][B*n][A]. */
+/* Replicated-critic data parallelism, for batches whose critic fits the persistent chain (B * n_agents <= 80, as
+ * coma_smac's B = 8 at MMM2's 10 agents): every rank passes the WHOLE sampled batch to mc_train_step and runs the
+ * critic's T steps on it (identical on every rank: no per-step exchange, coma_learner.py:118-139 unchanged), and
+ * the actor (coma_learner.py:52-83) on episodes [lo, hi) only; the agent gradient + sums are then summed with ONE
+ * all-reduce (the mc_set_data_parallel callback or mc_comm_attach communicator, which must be set). hi <= lo turns
+ * it off (then an all-reduce set means the exchange mode above, on per-rank shards). */
+int mc_set_actor_shard(mc_handle* h, int32_t lo, int32_t hi);
+/* 0 = critic Q values the actor used [T][B*n][A]; 1 = TD(lambda) targets [T][B*n]; 2 = policy pi [T][rows][A]
+ * (rows = the actor's: its shard under mc_set_actor_shard). */
 int mc_copy_intermediate(mc_handle* h, int which, float* dst, int64_t* count, void* stream);
 
 #ifdef __cplusplus

@@ -108,6 +108,13 @@ int mq_comm_unique_id(uint8_t* id /* [MQ_COMM_ID_BYTES] */);
 int mq_comm_attach(mq_handle* h, const uint8_t* id, int32_t rank, int32_t world);
 int32_t mq_comm_world(const mq_handle* h);
 int mq_comm_detach(mq_handle* h);
+/* SURVEY.md §8b's mq_allreduce_attach(handle, ncclComm_t): attach a communicator the CALLER owns (an ncclComm_t,
+ * passed as void* so this header needs no RCCL include). The handle borrows it: detach / destroy leave it alive,
+ * and one communicator may serve several handles (QMIX and COMA learners of one process). mq_comm_create /
+ * mq_comm_free make and release one from a unique id for hosts without their own RCCL setup. */
+int mq_comm_use(mq_handle* h, void* nccl_comm);
+int mq_comm_create(const uint8_t* id, int32_t rank, int32_t world, void** nccl_comm);
+int mq_comm_free(void* nccl_comm);
 int mq_update_targets(mq_handle* h, void* stream);
 
 /* Copy an intermediate of the last mq_forward_backward into dst (device): 0 = online mac_out [t][b*n+a][A],

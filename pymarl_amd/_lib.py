@@ -31,7 +31,8 @@ EXPORTS = [
     "mc_create", "mc_destroy", "mc_param_offsets", "mc_bind", "mc_train_step", "mc_update_targets", "mc_policy",
     "mc_copy_intermediate", "mc_set_timing", "mc_phase_times", "mc_last_critic_path", "mq_comm_unique_id", "mq_comm_attach",
     "mq_comm_world", "mq_comm_detach", "mc_comm_attach", "mc_set_data_parallel", "mc_critic_forward",
-    "mc_critic_forward_workspace",
+    "mc_critic_forward_workspace", "mc_set_actor_shard", "mq_comm_use", "mq_comm_create", "mq_comm_free",
+    "mc_comm_use",
 ]
 
 # mc_allreduce_fn (include/mc_coma.h): int (*)(float* buf, int64_t count, void* stream, void* ctx)
@@ -88,6 +89,7 @@ HYP_NAMES = {0: "none", 1: "ws", 2: "lds", 3: "gemm"}
 MIX_NAMES = {0: "fast16", 1: "fast32", 2: "generic"}
 
 INLINE_IDS = 256   # MQ_INLINE_IDS: batches up to this size pass their episode ids in the kernel arguments
+COMM_ID_BYTES = 128   # MQ_COMM_ID_BYTES (ncclUniqueId)
 
 
 _LIB = None
@@ -148,6 +150,11 @@ def load(required=True):
         "mq_comm_detach": ([vp], ctypes.c_int),
         "mc_comm_attach": ([vp, vp, i32, i32], ctypes.c_int),
         "mc_set_data_parallel": ([vp, MC_ALLREDUCE_FN, vp, i32, vp, i64], ctypes.c_int),
+        "mc_set_actor_shard": ([vp, i32, i32], ctypes.c_int),
+        "mq_comm_use": ([vp, vp], ctypes.c_int),
+        "mq_comm_create": ([vp, i32, i32, ctypes.POINTER(vp)], ctypes.c_int),
+        "mq_comm_free": ([vp], ctypes.c_int),
+        "mc_comm_use": ([vp, vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

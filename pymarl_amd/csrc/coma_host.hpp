@@ -22,7 +22,7 @@ struct mc_handle {
   int* cstate;
   // actor workspace
   float *dL, *dHo, *pi, *ppart, *slab_fc2, *red_tmp, *norm_part;
-  int last_T = 0, last_R = 0;
+  int last_T = 0, last_R = 0, last_Rc = 0;
   bool timing = false;
   // persistent critic chain (coma_chain.hpp): off with MQ_COMA_CHAIN=0, or where cc_ok rejects the shape
   bool chain_env = true;
@@ -39,6 +39,10 @@ struct mc_handle {
   std::vector<float> dp_msum;
   ncclComm_t comm = nullptr;   // mc_comm_attach: native RCCL exchange steps
   float* comm_scratch = nullptr;
+  bool comm_owned = false;   // mc_comm_attach created it; mc_comm_use borrows the caller's
+  // mc_set_actor_shard: replicated-critic data parallelism (every rank runs the critic on the whole batch, the actor
+  // on episodes [shard_lo, shard_hi) with one all-reduce of the agent gradient); off while shard_hi <= shard_lo
+  int shard_lo = 0, shard_hi = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -57,6 +61,27 @@ int mc_allreduce_ws(mc_handle* h, float* ws_buf, int64_t n, hipStream_t s) {
   if (rc) return rc;
   MQ_HIP(hipMemcpyAsync(ws_buf, h->dp_scratch, n * sizeof(float), hipMemcpyDeviceToDevice, s));
   return MQ_OK;
+}
+
+// Episodes [lo, hi) of a batch as a batch of their own: the id slice, or for a dense batch (no ids) every field
+// pointer advanced by lo episodes.
+mq_replay shard_replay(const mc_config& c, const mq_replay& b, int lo, int hi) {
+  mq_replay s = b;
+  s.batch_size = hi - lo;
+  if (b.ep_ids_host) s.ep_ids_host = b.ep_ids_host + lo;
+  if (b.ep_ids) s.ep_ids = b.ep_ids + lo;
+  if (!b.ep_ids && !(b.ep_ids_host && b.batch_size <= MQ_INLINE_IDS)) {
+    const int64_t e = (int64_t)lo * b.t_stride, n = c.n_agents;
+    if (s.obs) s.obs += e * n * c.obs_dim;
+    if (s.state) s.state += e * c.state_dim;
+    if (s.actions) s.actions += e * n;
+    if (s.avail_actions) s.avail_actions += e * n * c.n_actions;
+    if (s.reward) s.reward += e;
+    if (s.terminated) s.terminated += e;
+    if (s.filled) s.filled += e;
+    s.n_episodes = b.n_episodes - lo;
+  }
+  return s;
 }
 
 int mc_agent_config(const mc_config& c, mq_config* a) {
@@ -211,7 +236,7 @@ int mc_destroy(mc_handle* h) {
   if (!h) return MQ_OK;
   if (h->ws) (void)hipFree(h->ws);
   if (h->chain_trace) (void)hipFree(h->chain_trace);
-  if (h->comm) (void)ncclCommDestroy(h->comm);
+  if (h->comm && h->comm_owned) (void)ncclCommDestroy(h->comm);
   if (h->comm_scratch) (void)hipFree(h->comm_scratch);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
@@ -258,12 +283,19 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   cd.dR = make_fastdiv((uint32_t)R);
   cd.dN = make_fastdiv((uint32_t)n);
 
+  const bool repl = h->shard_hi > h->shard_lo;
+  if (repl && (h->shard_lo < 0 || h->shard_hi > batch->batch_size))
+    return set_err(MQ_ERR_ARG, "actor shard [" + std::to_string(h->shard_lo) + ", " + std::to_string(h->shard_hi) +
+                                   ") outside the batch of " + std::to_string(batch->batch_size) + " episodes");
+  if (repl && !h->dp_fn)
+    return set_err(MQ_ERR_STATE, "a replicated critic needs an all-reduce for the actor (mc_set_data_parallel / "
+                                 "mc_comm_attach)");
   if (h->timing) MQ_HIP(hipEventRecord(h->ev[0], s));
   MQ_HIP(hipMemsetAsync(h->crec, 0, (size_t)T * 8 * sizeof(float), s));
   MQ_HIP(hipMemsetAsync(h->cstate, 0, 8 * sizeof(int), s));
   hipLaunchKernelGGL(coma_mask_kernel, dim3((T + 255) / 256), dim3(256), 0, s, cd, rp, h->msum);
   MQ_HIP(hipGetLastError());
-  const bool dp = h->dp_fn != nullptr;
+  const bool dp = h->dp_fn != nullptr && !repl;   // exchange mode: the critic steps are summed over the ranks
   if (dp) {   // global per-step mask sums: every rank normalises by them and skips the same steps
     if (h->dp_scratch_n < 8LL * T) return set_err(MQ_ERR_ARG, "data-parallel scratch smaller than 8 * t_len");
     rc = mc_allreduce_ws(h, h->msum, T, s);
@@ -316,8 +348,11 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   }
   // ---- the actor's agent unroll over t < T (coma_learner.py:52-57), online net only. It reads nothing the critic
   // writes, so beside the persistent chain it runs on the side stream in the CUs the chain leaves idle.
-  mq_replay av = *batch;
+  // replicated critic: the actor trains this rank's episodes only (the critic above saw the whole batch)
+  mq_replay av = repl ? shard_replay(c, *batch, h->shard_lo, h->shard_hi) : *batch;
   av.t_len = T;
+  const Rep rpa = repl ? make_rep(&av) : rp;
+  const int qv_r0 = repl ? h->shard_lo * n : 0;   // this rank's first row in the critic's [T][B n][A] Q values
   Dims d = make_dims(ah, &av);
   const Lay L = make_lay(ah);
   Work w = ah->w;
@@ -327,10 +362,10 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   auto agent_forward = [&](hipStream_t st) -> int {
     const int rw_fwd = pick_rw(d.R, 512);
     if (rw_fwd == 1 && fused_fwd_ok(d.I, d.O, d.A, d.n, RT)) {
-      launch_fwd_fused(dim3(d.R, 1), st, d, rp, Pa, Pa, L, w);
+      launch_fwd_fused(dim3(d.R, 1), st, d, rpa, Pa, Pa, L, w);
       MQ_HIP(hipGetLastError());
     } else {
-      Fc1Prob p1{d, rp, Pa, Pa, ah->off[MQ_P_FC1_W], ah->off[MQ_P_FC1_B], w.X1, w.XIN, RT};
+      Fc1Prob p1{d, rpa, Pa, Pa, ah->off[MQ_P_FC1_W], ah->off[MQ_P_FC1_B], w.X1, w.XIN, RT};
       MQ_HIP(launch_gemm(p1, (int)RT, 2 * mq::H, 1, st));
       GiProb p2{w.X1, Pa, Pa, ah->off[MQ_P_RNN_W_IH], ah->off[MQ_P_RNN_B_IH], w.GI, RT};
       MQ_HIP(launch_gemm(p2, (int)RT, mq::G3, 1, st));
@@ -453,9 +488,9 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   // policy, baseline, advantage, loss sums and dLogits (coma_learner.py:59-77, basic_controller.py:53-73)
   const int npol = (int)((RT + 3) / 4);
   const float eps = epsilon, omeps = (float)(1.0 - (double)epsilon);
-  hipLaunchKernelGGL(coma_policy_kernel, dim3(npol), dim3(256), 0, s, d, rp, (const float*)w.Q,
-                     (const float*)h->qvals, eps, omeps, (int)(c.mask_before_softmax != 0), h->Ap, h->dL, h->pi,
-                     h->ppart);
+  hipLaunchKernelGGL(coma_policy_kernel, dim3(npol), dim3(256), 0, s, d, rpa, (const float*)w.Q,
+                     (const float*)h->qvals, R, qv_r0, eps, omeps, (int)(c.mask_before_softmax != 0), h->Ap, h->dL,
+                     h->pi, h->ppart);
   MQ_HIP(hipGetLastError());
   // BPTT with the dense output gradient
   {
@@ -466,9 +501,9 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   int nblk_bwd = (d.R + rw_bwd - 1) / rw_bwd;
   const size_t dyn = ((size_t)2 * d.A * mq::H + d.A) * sizeof(float);
   if (rw_bwd == 1)
-    hipLaunchKernelGGL((gru_bwd_kernel<1, 0, true>), dim3(nblk_bwd), dim3(512), dyn, s, d, rp, Pa, L, w, ah->len_rnn);
+    hipLaunchKernelGGL((gru_bwd_kernel<1, 0, true>), dim3(nblk_bwd), dim3(512), dyn, s, d, rpa, Pa, L, w, ah->len_rnn);
   else
-    hipLaunchKernelGGL((gru_bwd_kernel<2, 0, true>), dim3(nblk_bwd), dim3(512), dyn, s, d, rp, Pa, L, w, ah->len_rnn);
+    hipLaunchKernelGGL((gru_bwd_kernel<2, 0, true>), dim3(nblk_bwd), dim3(512), dyn, s, d, rpa, Pa, L, w, ah->len_rnn);
   MQ_HIP(hipGetLastError());
   {
     Dx1Prob p{w.dGI, Pa + ah->off[MQ_P_RNN_W_IH], w.X1, w.dP1, RT};
@@ -510,7 +545,7 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
     MQ_HIP(hipGetLastError());
     nnorm = rb.b2;
   }
-  if (dp) {   // the agent gradient + loss / mask sums, then the norm partials of the summed gradient
+  if (dp || repl) {   // the agent gradient + loss / mask sums, then the norm partials of the summed gradient
     rc = mc_allreduce(h, h->agrad, h->Pa + MQ_NSUMS, s);
     if (rc) return rc;
     nnorm = 256;
@@ -531,7 +566,8 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   if (h->timing) MQ_HIP(hipEventRecord(h->ev[3], s));
   h->last_path = chained ? 1 : 0;
   h->last_T = T;
-  h->last_R = R;
+  h->last_R = d.R;   // the rows of pi (the actor's); qvals / targets keep the critic's R rows
+  h->last_Rc = R;
   return MQ_OK;
 }
 
@@ -554,6 +590,14 @@ static int mc_rccl_allreduce(float* buf, int64_t count, void* stream, void* ctx)
   return ncclAllReduce(buf, buf, (size_t)count, ncclFloat, ncclSum, h->comm, (hipStream_t)stream) == ncclSuccess ? 0 : 1;
 }
 
+int mc_set_actor_shard(mc_handle* h, int32_t lo, int32_t hi) {
+  if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
+  if (hi > lo && (lo < 0 || hi > h->cfg.max_batch)) return set_err(MQ_ERR_ARG, "mc_set_actor_shard: bad episode range");
+  h->shard_lo = hi > lo ? lo : 0;
+  h->shard_hi = hi > lo ? hi : 0;
+  return MQ_OK;
+}
+
 int mc_comm_attach(mc_handle* h, const uint8_t* id, int32_t rank, int32_t world) {
   if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
   if (h->comm) return set_err(MQ_ERR_STATE, "a communicator is already attached");
@@ -561,6 +605,20 @@ int mc_comm_attach(mc_handle* h, const uint8_t* id, int32_t rank, int32_t world)
   if (!h->comm_scratch) MQ_HIP(hipMalloc(&h->comm_scratch, n * sizeof(float)));
   const int rc = comm_init(&h->comm, id, rank, world);
   if (rc) return rc;
+  h->comm_owned = true;
+  return mc_set_data_parallel(h, mc_rccl_allreduce, h, rank, h->comm_scratch, n);
+}
+
+int mc_comm_use(mc_handle* h, void* comm) {
+  if (!h || !comm) return set_err(MQ_ERR_ARG, "NULL handle or communicator");
+  if (h->comm) return set_err(MQ_ERR_STATE, "a communicator is already attached");
+  int rank = 0;
+  const ncclResult_t r = ncclCommUserRank((ncclComm_t)comm, &rank);
+  if (r != ncclSuccess) return set_err(MQ_ERR_ARG, std::string("ncclCommUserRank: ") + ncclGetErrorString(r));
+  const int64_t n = 8LL * h->cfg.max_seq;
+  if (!h->comm_scratch) MQ_HIP(hipMalloc(&h->comm_scratch, n * sizeof(float)));
+  h->comm = (ncclComm_t)comm;
+  h->comm_owned = false;
   return mc_set_data_parallel(h, mc_rccl_allreduce, h, rank, h->comm_scratch, n);
 }
 
@@ -600,12 +658,12 @@ int mc_policy(float* logits, const int32_t* avail, int32_t rows, int32_t n_actio
 
 int mc_copy_intermediate(mc_handle* h, int which, float* dst, int64_t* count, void* stream) {
   if (!h || h->last_T <= 0) return set_err(MQ_ERR_STATE, "no COMA train step has run");
-  const int64_t TR = (int64_t)h->last_T * h->last_R;
+  const int64_t TR = (int64_t)h->last_T * h->last_R, TRc = (int64_t)h->last_T * h->last_Rc;
   const float* src;
   int64_t cnt;
   switch (which) {
-    case 0: src = h->qvals; cnt = TR * h->cfg.n_actions; break;
-    case 1: src = h->tgt; cnt = TR; break;
+    case 0: src = h->qvals; cnt = TRc * h->cfg.n_actions; break;
+    case 1: src = h->tgt; cnt = TRc; break;
     case 2: src = h->pi; cnt = TR * h->cfg.n_actions; break;
     default: return set_err(MQ_ERR_ARG, "unknown COMA intermediate id");
   }

@@ -712,8 +712,11 @@ __global__ __launch_bounds__(256) void coma_capply_kernel(CritArgs a) {
 // and the backward of sum(adv log pi m) down to the logits (unnormalised: the apply divides by sum m).
 // Writes dL [RT][Ap] (pad columns zero), pi [RT][A], per-block sums:
 // [0] -sum adv log pi m, [1] sum m, [2] sum adv m, [3] sum max(pi) m.
+// qvals [T][qv_R][A]: the critic's Q values, this launch's rows starting at row qv_r0 (an actor shard of a
+// replicated critic; else qv_R = d.R, qv_r0 = 0).
 __global__ __launch_bounds__(256) void coma_policy_kernel(Dims d, Rep rp, const float* __restrict__ logits,
-                                                          const float* __restrict__ qvals, float eps, float omeps,
+                                                          const float* __restrict__ qvals, int qv_R, int qv_r0,
+                                                          float eps, float omeps,
                                                           int mbs,
                                                           int Ap, float* __restrict__ dL, float* __restrict__ pi_out,
                                                           float* __restrict__ part) {
@@ -739,7 +742,7 @@ __global__ __launch_bounds__(256) void coma_policy_kernel(Dims d, Rep rp, const 
     if (!av) out = 0.0f;                                   // mac_out[avail == 0] = 0
     const float s = wave_sum(out);
     const float p = (av && s > 0.0f) ? out / s : 0.0f;     // renormalise; 0/0 rows -> 0 (coma_learner.py:60-62)
-    const float qv = on ? qvals[tr * A + lane] : 0.0f;
+    const float qv = on ? qvals[((int64_t)t * qv_R + qv_r0 + r) * A + lane] : 0.0f;
     const float baseline = wave_sum(p * qv);
     const int at = (int)rp.actions[slot * n + ag];
     const float q_taken = __shfl(qv, at, 64);

@@ -45,7 +45,9 @@ inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_
 // the chain then owns two SIMDs outright and the producers' f32 MFMAs (which hold the SIMD's FMA datapath) run on
 // the other two instead of beside every chain wave (measured slower: the producers, two per SIMD, then set the
 // step), 2048 the next step's W2 lookup issued at the top of the step with a 4-slot input rotation, 4096 four
-// accumulator pairs in the W_hh^T mat-vec.
+// accumulator pairs in the W_hh^T mat-vec, 8192 per-phase cycle budget of the chain step (s_memtime stamps of chain
+// wave 0: inputs + gate math + LDS stores | barrier | LDS reads of dgh | W_hh^T FMAs | DPP quad reduction + W2
+// lookup), summed over the steps into w.slab_mix[32 * block + 17 ..] (diagnostic, scripts/chain_micro.hip).
 template <int VAR = 0>
 __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
                                                             Work w, int64_t slab_len, int64_t slab1_len) {
@@ -55,6 +57,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
   constexpr bool kSplit = (VAR & 1024) != 0;
   constexpr bool kEarlyW2 = (VAR & 2048) != 0;
   constexpr bool kAcc4 = (VAR & 4096) != 0;
+  constexpr bool kStamp = (VAR & 8192) != 0;
   const bool chain = kSplit ? ((tid >> 7) & 1) == 0 : tid < 256;
   // role-local thread id 0..255 (wave-uniform role; lanes of a quad stay in one wave)
   const int lt = kSplit ? ((tid & 127) | ((tid >> 8) << 7)) : (tid & 255), k = lt >> 2, q = lt & 3;
@@ -130,9 +133,12 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     const float m0 = q == 0 ? 1.0f : 0.0f, m1 = q == 1 ? 1.0f : 0.0f, m2 = q == 2 ? 1.0f : 0.0f;
     const float m3 = q == 3 ? 1.0f : 0.0f;
     float carry = 0.0f, db_i = 0.0f, db_h = 0.0f;   // bias grads: this lane's component q of b_ih / b_hh
+    uint64_t ph[5] = {0, 0, 0, 0, 0};   // kStamp: cycles per phase, summed over the steps
     // ahead: the slot whose loads are issued this step (t - 1 with two slots; t - 2 with three, VAR 256, so every
     // load has two chain steps of latency instead of one); nxt: the next step's slot, whose w2 is looked up here
     auto step = [&](int t, const In& cur, In& nxt, In& ahead, int dist) {
+      uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+      if (kStamp) s0 = __builtin_amdgcn_s_memtime();
       load(t - dist, ahead);
       // VAR 2048: the next step's W2[a][k] lookup is issued here, a whole step before its use, instead of at the
       // end of the step where its LDS latency sat on the dh chain (nxt was loaded two steps ago: 4-slot rotation)
@@ -156,9 +162,33 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       db_i = fmaf(1.0f - m3, mine_i, db_i);
       db_h = fmaf(1.0f - m3, mine_h, db_h);
       const float cz = dh * gz;
+      if (kStamp) s1 = __builtin_amdgcn_s_memtime();
       lds_barrier();
       // dh_{t-1} = dh * z + W_hh^T dgh
       const f32x4* dg4 = (const f32x4*)(&S.gh[cb][p][48 * q]);
+      if (kStamp) {   // the same arithmetic as below, with the LDS reads completed before the FMAs
+        s2 = __builtin_amdgcn_s_memtime();
+        f32x4 dv[12];
+#pragma unroll
+        for (int c4 = 0; c4 < 12; ++c4) dv[c4] = dg4[c4];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        s3 = __builtin_amdgcn_s_memtime();
+        f32x2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
+#pragma unroll
+        for (int c4 = 0; c4 < 12; ++c4) {
+          a01 = pk_fma(wT[2 * c4], f32x2{dv[c4][0], dv[c4][1]}, a01);
+          a23 = pk_fma(wT[2 * c4 + 1], f32x2{dv[c4][2], dv[c4][3]}, a23);
+        }
+        const float part = (a01.x + a01.y) + (a23.x + a23.y);
+        asm volatile("" :: "v"(part));
+        s4 = __builtin_amdgcn_s_memtime();
+        carry = cz + quad_sum(part);
+        lookup_w2(nxt);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint64_t s5 = __builtin_amdgcn_s_memtime();
+        ph[0] += s1 - s0; ph[1] += s2 - s1; ph[2] += s3 - s2; ph[3] += s4 - s3; ph[4] += s5 - s4;
+        return;
+      }
       if (kAcc4) {   // VAR 4096: four accumulator pairs, dependency chains of 6 instead of 12
         f32x2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f}, a2 = {0.0f, 0.0f}, a3 = {0.0f, 0.0f};
 #pragma unroll
@@ -240,6 +270,11 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       if (t >= 0) step(t, sa, sb, sb, 1);
     }
     if (VAR & 128) __builtin_amdgcn_s_setprio(0);
+    if (kStamp && tid == 0) {
+      uint64_t* st = (uint64_t*)w.slab_mix + 32 * blockIdx.x;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) st[17 + i] = ph[i];
+    }
     lds_barrier();   // producer tail: chunk 0 (2 barriers)
     lds_barrier();
     if (q < 3) { slab[o_bi + q * H + k] = db_i; slab[o_bh + q * H + k] = db_h; }

@@ -60,7 +60,9 @@ struct FusedLds {
 // 128 chain waves without priority, 256 gathers two chunks ahead, 512 producer work spread over all 16 phases,
 // 1024 target chain above the online chain,
 // 4 producers idle (recurrence alone on stale gates), 8 per-phase cycle bins, 16 no obs loads, 32 no X1/XIN stores,
-// 64 prologue milestone stamps.
+// 64 prologue milestone stamps, 2048 per-phase cycle budget of the chain step (s_memtime stamps of wave 0: LDS reads
+// of h_{t-1} and the input gate | W_hh FMAs | DPP quad reductions | gate math + stores | barrier), summed over the
+// steps into w.slab_mix[16 * block + 8 ..] (diagnostic, scripts/chain_micro.hip).
 // NG: obs gather slots per producer thread (16 * O <= 256 * NG); the host picks the smallest instantiation
 // (launch_fwd_fused) because every slot holds two VGPRs across the whole T loop.
 template <int VAR = 0, int NG = FGATHER>
@@ -178,12 +180,38 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const float bsel = m0 * bhr + m1 * bhz;
     float hprev = 0.0f;   // h_{t-1}[j]: every lane of the quad computes unit j's h, so it never re-reads LDS
     const uint32_t hlo = q == 0 ? ((uint32_t)r * H + j) * 4 : kDrop, glo = ((uint32_t)r * (4 * H) + q * H + j) * 4;
+    uint64_t ph[5] = {0, 0, 0, 0, 0};
     auto step = [&](int t) {
       const int p = t & (FCH - 1), c = t / FCH;
       const float* hb = t == 0 ? S.h0 : S.hs[((t - 1) / FCH) & 1][(t - 1) & (FCH - 1)];
+      uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+      if (VAR & 2048) s0 = __builtin_amdgcn_s_memtime();
       const float own = S.gi[c & 1][p][gcol];   // issued with the h reads below (same LDS latency window)
       float sr, sz, sn;
-      {
+      if (VAR & 2048) {   // the same arithmetic with the LDS reads completed first
+        const f32x4* hv4 = (const f32x4*)(&hb[16 * q]);
+        f32x4 hv[4];
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) hv[k4] = hv4[k4];
+        asm volatile("s_waitcnt lgkmcnt(0)" :: "v"(own) : "memory");
+        s1 = __builtin_amdgcn_s_memtime();
+        f32x2 ar = {0.0f, 0.0f}, az = {0.0f, 0.0f}, an = {0.0f, 0.0f};
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+          const f32x2 h01 = {hv[k4][0], hv[k4][1]}, h23 = {hv[k4][2], hv[k4][3]};
+          ar = pk_fma(wr[2 * k4], h01, ar); ar = pk_fma(wr[2 * k4 + 1], h23, ar);
+          az = pk_fma(wz[2 * k4], h01, az); az = pk_fma(wz[2 * k4 + 1], h23, az);
+          an = pk_fma(wn[2 * k4], h01, an); an = pk_fma(wn[2 * k4 + 1], h23, an);
+        }
+        const float pr = ar.x + ar.y, pz = az.x + az.y, pn = an.x + an.y;
+        asm volatile("" :: "v"(pr), "v"(pz), "v"(pn));
+        s2 = __builtin_amdgcn_s_memtime();
+        sr = quad_sum(pr);
+        sz = quad_sum(pz);
+        sn = quad_sum(pn);
+        asm volatile("" :: "v"(sr), "v"(sz), "v"(sn));
+        s3 = __builtin_amdgcn_s_memtime();
+      } else {
         const f32x4* hv4 = (const f32x4*)(&hb[16 * q]);
         f32x2 ar = {0.0f, 0.0f}, az = {0.0f, 0.0f}, an = {0.0f, 0.0f};
 #pragma unroll
@@ -211,7 +239,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         buf_st(buf_rsrc(Hz + (int64_t)t * RH), hlo, h1);   // wave-uniform bases; lanes q != 0 drop the h store
         buf_st(buf_rsrc(w.Gates + (int64_t)t * (4 * RH)), glo, fmaf(m0, rg, fmaf(m1, zg, fmaf(m2, ng, m3 * ghn))));
       }
+      if (VAR & 2048) s4 = __builtin_amdgcn_s_memtime();
       lds_barrier();
+      if (VAR & 2048) {
+        const uint64_t s5 = __builtin_amdgcn_s_memtime();
+        ph[0] += s1 - s0; ph[1] += s2 - s1; ph[2] += s3 - s2; ph[3] += s4 - s3; ph[4] += s5 - s4;
+      }
     };
     // the chains of both nets issue ahead of every producer wave on the CU (the online workgroups are older and
     // would otherwise win arbitration against the target chain too); VAR 128 turns this off for A/B runs
@@ -243,6 +276,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       for (int t = 0; t < Tp; ++t) step(t);
     }
     __builtin_amdgcn_s_setprio(0);
+    if ((VAR & 2048) && tid == 0) {
+#pragma unroll
+      for (int i = 0; i < 5; ++i) ((uint64_t*)w.slab_mix)[16 * (blockIdx.y * gridDim.x + blockIdx.x) + 8 + i] = ph[i];
+    }
     if ((VAR & 2) && tid == 0) {   // diagnostic only: shader cycles and 100 MHz ticks of the whole T loop
       const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
       ((uint64_t*)w.slab_mix)[2 * (blockIdx.y * gridDim.x + blockIdx.x)] = c1 - c0;

@@ -91,8 +91,9 @@ struct mq_handle {
   int dwh_split = getenv("MQ_DWH_SPLIT") ? atoi(getenv("MQ_DWH_SPLIT")) : 8;   // m-slices of the dW_hyper pass
   bool generic_mix = getenv("MQ_GENERIC_MIX") != nullptr;   // A/B switch: mix_kernel instead of mix_fast_kernel
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
-  ncclComm_t comm = nullptr;   // mq_comm_attach: the library all-reduces the grad buffer itself
+  ncclComm_t comm = nullptr;   // mq_comm_attach / mq_comm_use: the library all-reduces the grad buffer itself
   int comm_world = 0;
+  bool comm_owned = false;     // mq_comm_attach created it (freed on detach); mq_comm_use borrows the caller's
   // A/B switch, off by default: dW_hyper on a side stream beside the fused BPTT (dwh_kernel.hpp). Measured at cfg2
   // (r01l): the co-resident dwh_side waves slow the BPTT chain 92.7 -> 105.6 us, the step 238 -> 264 us
   bool dwh_overlap = getenv("MQ_DWH_OVERLAP") && atoi(getenv("MQ_DWH_OVERLAP")) != 0;
@@ -386,7 +387,7 @@ int mq_destroy(mq_handle* h) {
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->side) (void)hipStreamDestroy(h->side);
   if (h->ws) (void)hipFree(h->ws);
-  if (h->comm) (void)ncclCommDestroy(h->comm);
+  if (h->comm && h->comm_owned) (void)ncclCommDestroy(h->comm);
   delete h;
   return MQ_OK;
 }
@@ -685,6 +686,33 @@ int mq_comm_attach(mq_handle* h, const uint8_t* id, int32_t rank, int32_t world)
   const int rc = comm_init(&h->comm, id, rank, world);
   if (rc) return rc;
   h->comm_world = world;
+  h->comm_owned = true;
+  return MQ_OK;
+}
+
+int mq_comm_create(const uint8_t* id, int32_t rank, int32_t world, void** comm) {
+  if (!comm) return set_err(MQ_ERR_ARG, "NULL comm");
+  ncclComm_t c = nullptr;
+  const int rc = comm_init(&c, id, rank, world);
+  if (rc) return rc;
+  *comm = (void*)c;
+  return MQ_OK;
+}
+
+int mq_comm_free(void* comm) {
+  if (comm) (void)ncclCommDestroy((ncclComm_t)comm);
+  return MQ_OK;
+}
+
+int mq_comm_use(mq_handle* h, void* comm) {
+  if (!h || !comm) return set_err(MQ_ERR_ARG, "NULL handle or communicator");
+  if (h->comm) return set_err(MQ_ERR_STATE, "a communicator is already attached (mq_comm_detach first)");
+  int world = 0;
+  const ncclResult_t r = ncclCommCount((ncclComm_t)comm, &world);
+  if (r != ncclSuccess) return set_err(MQ_ERR_ARG, std::string("ncclCommCount: ") + ncclGetErrorString(r));
+  h->comm = (ncclComm_t)comm;
+  h->comm_world = world;
+  h->comm_owned = false;
   return MQ_OK;
 }
 
@@ -692,9 +720,10 @@ int32_t mq_comm_world(const mq_handle* h) { return h ? h->comm_world : 0; }
 
 int mq_comm_detach(mq_handle* h) {
   if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
-  if (h->comm) (void)ncclCommDestroy(h->comm);
+  if (h->comm && h->comm_owned) (void)ncclCommDestroy(h->comm);
   h->comm = nullptr;
   h->comm_world = 0;
+  h->comm_owned = false;
   return MQ_OK;
 }
 

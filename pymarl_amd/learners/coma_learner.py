@@ -9,9 +9,17 @@ hand-written HIP kernels (include/mc_coma.h, pymarl_amd/csrc/coma_kernels.hpp); 
 There is no CPU path. One synchronisation per train(): the stats read-back the target update needs.
 
 Data parallel (not in the reference): with `args.learner_dp = True` and torch.distributed initialised,
-each rank trains its shard of the global sample and the library calls back into `dist.all_reduce` at every exchange
-step (the global per-step mask sums, each live critic step's gradient, the critic stat sums, the agent gradient);
-see include/mc_coma.h, mc_set_data_parallel. T = 180 critic steps mean 180 small all-reduces per train.
+every rank passes the SAME global sample to train() and trains its share of it, in one of two modes
+(`args.coma_dp_mode`, default "auto"):
+* "replicated" (auto when B * n_agents <= 80, the persistent critic chain's limit; coma_smac's B = 8 at MMM2's 10
+  agents): every rank runs the critic's T steps on the whole batch — identical on every rank, so no per-step
+  exchange — and the actor on its own episodes, with ONE all-reduce of the agent gradient (mc_set_actor_shard);
+* "exchange": every rank trains its shard, and the library sums the global per-step mask sums, each live critic
+  step's gradient, the critic stat sums and the agent gradient across ranks (T + 3 all-reduces per train;
+  include/mc_coma.h, mc_set_data_parallel).
+Under an RCCL process group the exchanges run on the library's own communicator (mc_comm_attach, the id broadcast
+over torch.distributed once), in stream order with no Python callback; other backends call back into
+`dist.all_reduce`.
 
 Reference quirk kept on purpose: the actor reads `mac.action_selector.epsilon`, the value the last rollout call of
 select_actions left there (basic_controller.py:64-67).
@@ -27,8 +35,11 @@ from torch.optim import RMSprop
 from .. import _lib
 from ..modules.critics.coma import COMACritic
 from ..modules.flat import pack, rebind
+from .dp import broadcast_comm_id, dp_world, native_comm_wanted, shard_batch, shard_bounds
 from .q_learner import replay_view
 from ..components.episode_buffer import is_replay_view
+
+CC_MAXR = 80   # coma_chain.hpp: most critic rows (B * n_agents) the persistent chain takes
 
 
 def make_coma_config(args, input_dim, max_batch, max_seq):
@@ -128,12 +139,17 @@ class COMALearner:
             P = _lib.ptr
             _lib.check(h.lib.mc_bind(h.h, P(self._agent), P(self._agrad), P(self._asq), P(self._critic),
                                      P(self._tcritic), P(self._cgrad), P(self._csq), P(self._stats)))
+            h.native = False
             if self._dp_active():
-                self._dp_scratch = th.zeros(8 * T, dtype=th.float32, device=self._critic.device)
-                self._dp_cb = _lib.MC_ALLREDUCE_FN(self._allreduce)
-                import torch.distributed as dist
-                _lib.check(h.lib.mc_set_data_parallel(h.h, self._dp_cb, None, dist.get_rank(), P(self._dp_scratch),
-                                                      self._dp_scratch.numel()))
+                rank, world = dp_world()
+                if native_comm_wanted(self._critic.device):
+                    _lib.check(h.lib.mc_comm_attach(h.h, broadcast_comm_id(h.lib, self._critic.device), rank, world))
+                    h.native = True
+                else:
+                    self._dp_scratch = th.zeros(8 * T, dtype=th.float32, device=self._critic.device)
+                    self._dp_cb = _lib.MC_ALLREDUCE_FN(self._allreduce)
+                    _lib.check(h.lib.mc_set_data_parallel(h.h, self._dp_cb, None, rank, P(self._dp_scratch),
+                                                          self._dp_scratch.numel()))
             self._handle, self._handle_key = h, (need_b, T)
         return self._handle
 
@@ -142,6 +158,23 @@ class COMALearner:
             return False
         import torch.distributed as dist
         return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+    def dp_mode(self, batch_size):
+        """None (not data parallel), "replicated" or "exchange" for a global batch of `batch_size` episodes."""
+        if not self._dp_active():
+            return None
+        mode = getattr(self.args, "coma_dp_mode", "auto")
+        if mode == "auto":
+            mode = "replicated" if batch_size * self.n_agents <= CC_MAXR else "exchange"
+        if mode not in ("replicated", "exchange"):
+            raise ValueError("coma_dp_mode {!r} not recognised".format(mode))
+        return mode
+
+    def collective(self):
+        """"rccl-native", "torch.distributed" (callbacks) or None, for the last handle."""
+        if not self._dp_active():
+            return None
+        return "rccl-native" if (self._handle is not None and self._handle.native) else "torch.distributed"
 
     def _allreduce(self, ptr, count, stream, ctx):
         """mc_allreduce_fn: sum `count` floats of one of our own device buffers over the ranks, in stream order."""
@@ -160,6 +193,17 @@ class COMALearner:
     def train(self, batch, t_env: int, episode_num: int):
         _lib.require_gpu(self._agent)
         h = self._get_handle(batch)
+        mode = self.dp_mode(batch.batch_size)
+        if mode is not None:
+            rank, world = dp_world()
+            if mode == "replicated":   # the critic on the whole batch, the actor on this rank's episodes
+                lo, hi = shard_bounds(batch.batch_size, rank, world)
+                if hi <= lo:
+                    raise ValueError("replicated COMA critic: {} episodes for {} ranks".format(batch.batch_size, world))
+                _lib.check(h.lib.mc_set_actor_shard(h.h, lo, hi))
+            else:                      # exchange: this rank's shard through every step, summed in the library
+                _lib.check(h.lib.mc_set_actor_shard(h.h, 0, 0))
+                batch = shard_batch(batch, rank, world)
         rep, keep = replay_view(batch)
         eps = float(self.mac.action_selector.epsilon)
         _lib.check(h.lib.mc_train_step(h.h, ctypes.byref(rep), ctypes.c_float(eps), _lib.stream_ptr()))
@@ -244,6 +288,7 @@ class COMALearner:
         _lib.check(h.lib.mc_copy_intermediate(h.h, which, None, ctypes.byref(cnt), None))
         out = th.empty(cnt.value, dtype=th.float32, device=self._agent.device)
         _lib.check(h.lib.mc_copy_intermediate(h.h, which, _lib.ptr(out), ctypes.byref(cnt), _lib.stream_ptr()))
+        B = cnt.value // (T * n * (1 if which == 1 else A))   # pi has the actor's episodes (its shard when replicated)
         if which == 1:
             return out.view(T, B, n).permute(1, 0, 2)
         return out.view(T, B, n, A).permute(1, 0, 2, 3)

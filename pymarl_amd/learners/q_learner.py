@@ -9,6 +9,9 @@ device buffers. There is no CPU path: a learner that is not on a HIP device rais
 Data parallel: with `args.learner_dp = True` and torch.distributed initialised (RCCL, one process
 per GPU), each rank trains its shard of the sampled episodes, the unnormalised gradient buffer (+ the loss/mask
 sums in its tail) is summed with ONE all_reduce, and every rank then applies the identical normalised update.
+Under an RCCL process group the learner attaches the library's own communicator (mq_comm_attach, the id broadcast
+over torch.distributed once): the all-reduce is then issued inside mq_forward_backward, in stream order, and a
+train step makes no Python call between its kernels. Other backends (gloo) all-reduce from Python (dp.py).
 """
 from __future__ import annotations
 
@@ -24,7 +27,7 @@ from torch.optim import RMSprop
 from .. import _lib
 from ..components.episode_buffer import is_replay_view
 from ..modules.flat import pack, rebind
-from .dp import allreduce_grad_buffer
+from .dp import allreduce_grad_buffer, broadcast_comm_id, dp_world, native_comm_wanted
 from ..modules.mixers.qmix import QMixer
 from ..modules.mixers.vdn import VDNMixer
 
@@ -207,6 +210,11 @@ class QLearner:
             _lib.check(h.lib.mq_bind(h.h, _lib.ptr(self._online), _lib.ptr(self._target), _lib.ptr(self._grad),
                                      _lib.ptr(self._sq), _lib.ptr(self._stats), _lib.ptr(self._curmax)))
             h.dp_on = False
+            h.native = False
+            if self._dp_active() and native_comm_wanted(self._online.device):
+                rank, world = dp_world()
+                _lib.check(h.lib.mq_comm_attach(h.h, broadcast_comm_id(h.lib, self._online.device), rank, world))
+                h.native = True
             if h.n_params != self.n_params:
                 raise _lib.MQError("parameter layout mismatch: library {} vs modules {}".format(h.n_params,
                                                                                               self.n_params))
@@ -226,8 +234,8 @@ class QLearner:
             h.dp_on = want
         rep, keep = replay_view(batch)
         lib, s = h.lib, _lib.stream_ptr()
-        _lib.check(lib.mq_forward_backward(h.h, ctypes.byref(rep), s))
-        if dp:
+        _lib.check(lib.mq_forward_backward(h.h, ctypes.byref(rep), s))   # + the native all-reduce when attached
+        if dp and not h.native:
             allreduce_grad_buffer(self._grad)
         _lib.check(lib.mq_apply(h.h, s))
         self._opt_steps += 1
@@ -293,6 +301,13 @@ class QLearner:
         self._relink()
 
     # -- extras (parity / diagnostics) -----------------------------------------------------------------------
+    def collective(self):
+        """How a data-parallel step sums the gradient buffer: "rccl-native" (the library's communicator),
+        "torch.distributed", or None (not data parallel)."""
+        if not self._dp_active():
+            return None
+        return "rccl-native" if (self._handle is not None and self._handle.native) else "torch.distributed"
+
     def last_stats(self):
         """dict of the last step's stats (loss, grad_norm, td_error_abs, q_taken_mean, target_mean, mask_sum)."""
         st = self._stats.tolist()

@@ -1,0 +1,131 @@
+// Per-step cycle budget of the two fused recurrences at the cfg2 shape (B = 32, n = 8, T = 120), cache-hot, random
+// data: kernel time of production vs producers idle, and s_memtime phase stamps of the chain step (VAR 2048 in the
+// forward, 8192 in the BPTT; each the production schedule with the chain's LDS reads completed before its FMAs).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/chain_micro.hip -o scripts/chain_micro && scripts/chain_micro
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "../pymarl_amd/csrc/gru_bwd_fused.hpp"
+using namespace mq;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
+
+template <class F> float time_med(F f, int reps = 20, int rounds = 7) {
+  hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  f(); CK(hipDeviceSynchronize());
+  std::vector<float> v;
+  for (int r = 0; r < rounds; ++r) {
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i) f();
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b));
+    v.push_back(ms / reps * 1000.0f);
+  }
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+float* dev_rand(size_t n, float scale) {
+  std::vector<float> h(n);
+  for (auto& x : h) x = scale * ((rand() / (float)RAND_MAX) * 2.0f - 1.0f);
+  float* d; CK(hipMalloc(&d, n * 4)); CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+  return d;
+}
+
+int main(int argc, char** argv) {
+  int B = argc > 1 ? atoi(argv[1]) : 32, n = argc > 2 ? atoi(argv[2]) : 8, T = argc > 3 ? atoi(argv[3]) : 120;
+  const int A = 14, O = 80;
+  Dims d{};
+  d.n = n; d.A = A; d.O = O; d.S = 168; d.E = 32; d.I = O + A + n; d.NH = 32 * (n + 3);
+  d.B = B; d.Tp = T + 1; d.T = T; d.R = B * n; d.M = T * B; d.t_stride = T + 1;
+  d.last_action = 1; d.agent_id = 1; d.mixer = 2; d.double_q = 1; d.gamma = 0.99f;
+  d.dR = make_fastdiv(d.R); d.dN = make_fastdiv(n); d.dB = make_fastdiv(B);
+  d.dO = make_fastdiv(O); d.dI = make_fastdiv(d.I);
+  const int64_t RT = (int64_t)d.Tp * d.R;
+  Lay L{};
+  int64_t o = 0, sz[MQ_P_COUNT] = {};
+  sz[MQ_P_FC1_W] = 64 * d.I; sz[MQ_P_FC1_B] = 64; sz[MQ_P_RNN_W_IH] = 192 * 64; sz[MQ_P_RNN_W_HH] = 192 * 64;
+  sz[MQ_P_RNN_B_IH] = 192; sz[MQ_P_RNN_B_HH] = 192; sz[MQ_P_FC2_W] = A * 64; sz[MQ_P_FC2_B] = A;
+  for (int i = 0; i < MQ_P_COUNT; ++i) { L.o[i] = o; o += sz[i]; }
+  L.o[MQ_P_COUNT] = o;
+  float* P0 = dev_rand(o, 0.12f);
+  float* P1 = dev_rand(o, 0.12f);
+  Work w{};
+  CK(hipMalloc(&w.Hs, 2 * RT * 64 * 4)); CK(hipMalloc(&w.Gates, RT * 256 * 4)); CK(hipMalloc(&w.Q, 2 * RT * A * 4));
+  CK(hipMalloc(&w.X1, 2 * RT * 64 * 4)); CK(hipMemset(w.X1, 0, 2 * RT * 64 * 4));
+  CK(hipMalloc(&w.XIN, RT * d.I * 4)); CK(hipMemset(w.XIN, 0, RT * d.I * 4));
+  w.dch = dev_rand(RT, 0.1f);
+  CK(hipMalloc(&w.slab_mix, 32 * 8 * 2 * (int64_t)d.R));
+  const int64_t len_rnn = L.o[MQ_P_FC2_B] + A - L.o[MQ_P_RNN_W_IH], len1 = 64 * d.I + 64;
+  CK(hipMalloc(&w.slab_rnn, (int64_t)d.R * len_rnn * 4));
+  CK(hipMalloc(&w.slab_fc1, (int64_t)d.R * len1 * 4));
+  std::vector<int64_t> acts((int64_t)B * (T + 1) * n);
+  for (auto& a : acts) a = rand() % A;
+  int64_t* dacts; CK(hipMalloc(&dacts, acts.size() * 8)); CK(hipMemcpy(dacts, acts.data(), acts.size() * 8, hipMemcpyHostToDevice));
+  std::vector<int64_t> fl((int64_t)B * (T + 1), 1);
+  int64_t* dfl; CK(hipMalloc(&dfl, fl.size() * 8)); CK(hipMemcpy(dfl, fl.data(), fl.size() * 8, hipMemcpyHostToDevice));
+  Rep rp{};
+  rp.actions = dacts; rp.filled = dfl; rp.obs = dev_rand((int64_t)B * (T + 1) * n * O, 1.0f);
+  printf("B=%d n=%d T=%d rows=%d\n", B, n, T, d.R);
+
+  auto runf = [&](auto kern) {
+    return time_med([&] { hipLaunchKernelGGL(kern, dim3(d.R, 2), dim3(512), 0, 0, d, rp, (const float*)P0, (const float*)P1, L, w); });
+  };
+  auto fwd_budget = [&](const char* name) {
+    std::vector<uint64_t> sb(16 * 2 * (size_t)d.R);
+    CK(hipMemcpy(sb.data(), w.slab_mix, sb.size() * 8, hipMemcpyDeviceToHost));
+    const char* ph[5] = {"lds reads", "fmas", "quad sums", "gates+st", "barrier"};
+    printf("fwd %s cycles/step:", name);
+    double tot = 0;
+    for (int k = 0; k < 5; ++k) {
+      double c = 0;
+      for (int i = 0; i < 2 * d.R; ++i) c += sb[16 * i + 8 + k];
+      c /= 2.0 * d.R * d.Tp;
+      tot += c;
+      printf(" %s %.0f |", ph[k], c);
+    }
+    printf(" total %.0f\n", tot);
+  };
+  printf("fused fwd production %.1f us | producers idle %.1f us\n", runf(gru_fwd_fused_kernel<0, 5>),
+         runf(gru_fwd_fused_kernel<4, 5>));
+  printf("fused fwd stamped %.1f us | stamped, producers idle %.1f us\n", runf(gru_fwd_fused_kernel<2048, 5>),
+         runf(gru_fwd_fused_kernel<2052, 5>));
+  hipLaunchKernelGGL((gru_fwd_fused_kernel<2048, 5>), dim3(d.R, 2), dim3(512), 0, 0, d, rp, (const float*)P0, (const float*)P1, L, w);
+  CK(hipDeviceSynchronize());
+  fwd_budget("production");
+  hipLaunchKernelGGL((gru_fwd_fused_kernel<2052, 5>), dim3(d.R, 2), dim3(512), 0, 0, d, rp, (const float*)P0, (const float*)P1, L, w);
+  CK(hipDeviceSynchronize());
+  fwd_budget("producers idle");
+
+  const size_t dyn = (2 * A * 64 + A) * 4;
+  auto runb = [&](auto kern) {
+    return time_med([&] { hipLaunchKernelGGL(kern, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1); });
+  };
+  auto bwd_budget = [&](const char* name) {
+    std::vector<uint64_t> sb(32 * (size_t)d.R);
+    CK(hipMemcpy(sb.data(), w.slab_mix, sb.size() * 8, hipMemcpyDeviceToHost));
+    const char* ph[5] = {"gates+st", "barrier", "lds reads", "fmas", "quad sum+w2"};
+    printf("bwd %s cycles/step:", name);
+    double tot = 0;
+    for (int k = 0; k < 5; ++k) {
+      double c = 0;
+      for (int i = 0; i < d.R; ++i) c += sb[32 * i + 17 + k];
+      c /= (double)d.R * d.Tp;
+      tot += c;
+      printf(" %s %.0f |", ph[k], c);
+    }
+    printf(" total %.0f\n", tot);
+  };
+  printf("fused bwd production(768) %.1f us | producers idle(772) %.1f us\n", runb(gru_bwd_fused_kernel<768>),
+         runb(gru_bwd_fused_kernel<772>));
+  printf("fused bwd stamped %.1f us | stamped, producers idle %.1f us\n", runb(gru_bwd_fused_kernel<768 + 8192>),
+         runb(gru_bwd_fused_kernel<772 + 8192>));
+  hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 8192>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+  CK(hipDeviceSynchronize());
+  bwd_budget("production");
+  hipLaunchKernelGGL(gru_bwd_fused_kernel<772 + 8192>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+  CK(hipDeviceSynchronize());
+  bwd_budget("producers idle");
+  return 0;
+}
