@@ -357,7 +357,7 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   const Lay L = make_lay(ah);
   Work w = ah->w;
   w.dHo = h->dHo;
-  const int64_t RT = (int64_t)T * R;
+  const int64_t RT = (int64_t)T * d.R;   // the actor's rows (its shard under a replicated critic)
   const float* Pa = h->agent;
   auto agent_forward = [&](hipStream_t st) -> int {
     const int rw_fwd = pick_rw(d.R, 512);

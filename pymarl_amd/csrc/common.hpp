@@ -66,6 +66,14 @@ MQ_DEV float quad_xor1(float v) {
 MQ_DEV float quad_xor2(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
 }
+// Within each 16-lane DPP row: the value of lane (c + 8) mod 16 (row_ror:8, i.e. lane c ^ 8), and of lane 7 - c
+// within each 8-lane half (row_half_mirror; pairs lanes whose bit 2 differs).
+MQ_DEV float row_ror8(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x128, 0xF, 0xF, true));
+}
+MQ_DEV float row_half_mirror(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, true));
+}
 // Broadcast lane L of each quad to the whole quad.
 template <int L>
 MQ_DEV float quad_bcast(float v) {

@@ -34,7 +34,25 @@ struct BwdFusedLds {
   float dx1[FCH][H + 4];     // dX1 of the chunk being reduced
   float db1[4][H];           // fc1 bias-grad partials of the four lane groups
   float wih[G3][H + 1];      // W_ih (dX1's B operand); odd pitch: the four lane groups read rows 48 apart
+  float hnext[H];            // decoupled roles: h of the first step of the chunk processed last (fc2's operand)
+  int cflag[4];              // decoupled roles: per chain wave, the last step whose records it has published
+  int pflag[4];              // decoupled roles: per producer wave, the last chunk it has staged
 };
+
+// Wave-group rendezvous through LDS flags (decoupled roles, VAR 32768): the wave's earlier LDS stores complete
+// (lgkmcnt(0)), lane 0 publishes `cnt` in the wave's flag word, and the wave spins until all four flags of its
+// group reach `cnt`. LDS is one memory per CU and a wave's LDS operations complete in order, so a peer's records
+// are visible once its flag is. Unlike s_barrier it involves only the four waves of one role.
+MQ_DEV void group_sync(volatile int* flags, int wave_in_group, int lane, int cnt) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) flags[wave_in_group] = cnt;
+  // bounded: a wave that never publishes cannot hang the CU (the peers are LDS-local, so a healthy wait is a few
+  // hundred cycles; 2^22 polls is seconds)
+  for (int spins = 0; spins < (1 << 22); ++spins) {
+    const int f0 = flags[0], f1 = flags[1], f2 = flags[2], f3 = flags[3];
+    if (min(min(f0, f1), min(f2, f3)) >= cnt) break;
+  }
+}
 
 inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_fwd_ok(I, O, A, n, RT); }
 
@@ -47,7 +65,26 @@ inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_
 // step), 2048 the next step's W2 lookup issued at the top of the step with a 4-slot input rotation, 4096 four
 // accumulator pairs in the W_hh^T mat-vec, 8192 per-phase cycle budget of the chain step (s_memtime stamps of chain
 // wave 0: inputs + gate math + LDS stores | barrier | LDS reads of dgh | W_hh^T FMAs | DPP quad reduction + W2
-// lookup), summed over the steps into w.slab_mix[32 * block + 17 ..] (diagnostic, scripts/chain_micro.hip).
+// lookup), summed over the steps into w.slab_mix[32 * block + 17 ..] (diagnostic, scripts/chain_micro.hip), 16384
+// the K12 mat-vec layout (below), 32768 decoupled roles (below).
+//
+// Decoupled roles (VAR 32768). Default: every chain step ends in an s_barrier of all eight waves, so the chain waits
+// for the producer waves whenever a producer phase runs long (measured at cfg2: the barrier is 334 of 1,420 cycles a
+// step with the producers working, 105 with them idle). Decoupled: the four chain waves meet per step through LDS
+// flags (group_sync) and all eight waves meet once per 16-step chunk: at the end of the chain's chunk c the
+// producers have finished chunk c + 1 (its history buffer is then free for chunk c - 1) and start chunk c, whose
+// records are complete. A producer chunk runs its phases back to back (rows staged, one producer-group sync, dW_hh,
+// dW_ih, dX1, dW1, then fc2's 16 steps), in the default order of every accumulation: results are bitwise the
+// default schedule's.
+//
+// K12 layout of the W_hh^T mat-vec (VAR 16384). Default: lane (unit k, quarter q) sums 48 of the 192 dgh terms of
+// its own unit, so every chain lane reads 48 dgh values from LDS per step (48 KB a step for the four chain waves).
+// K12: lane c of 16-lane DPP row r16 sums the 12 terms k in [12c, 12c + 12) for the row's four units 4 r16 .. +3
+// (the same 48 FMAs, as 24 v_pk_fma_f32 with dgh[k] in both halves) and reads only those 12 values (12 KB a step).
+// The four partial sums per lane are reduce-scattered over the row with no selects: the W pairs are ordered per
+// lane (bit 3 of c picks which unit pair stays in A, bit 2 which unit leads each pair), so one row_ror:8 add (pairs
+// c, c ^ 8), one row_half_mirror add (pairs c, 7 - c: bit 2 differs) and the quad sum leave unit 4 r16 + 2 b3 + b2
+// = the lane's own quad index in all four lanes of the quad: the gate-math layout of the default path, unchanged.
 template <int VAR = 0>
 __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
                                                             Work w, int64_t slab_len, int64_t slab1_len) {
@@ -58,6 +95,8 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
   constexpr bool kEarlyW2 = (VAR & 2048) != 0;
   constexpr bool kAcc4 = (VAR & 4096) != 0;
   constexpr bool kStamp = (VAR & 8192) != 0;
+  constexpr bool kK12 = (VAR & 16384) != 0;
+  constexpr bool kDec = (VAR & 32768) != 0;
   const bool chain = kSplit ? ((tid >> 7) & 1) == 0 : tid < 256;
   // role-local thread id 0..255 (wave-uniform role; lanes of a quad stay in one wave)
   const int lt = kSplit ? ((tid & 127) | ((tid >> 8) << 7)) : (tid & 255), k = lt >> 2, q = lt & 3;
@@ -78,6 +117,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       if (tid + 512 * u < A * H) { w2_s[tid + 512 * u] = v[u]; dw2_s[tid + 512 * u] = 0.0f; }
   }
   for (int i = tid; i < A; i += 512) db2_s[i] = 0.0f;
+  if (tid < 4) { S.cflag[tid] = 0; S.pflag[tid] = 0; }
   // zero the history rows past Tp of the top (partial) chunk and the XIN padding
   for (int e = tid; e < 2 * FCH * BRP; e += 512) { (&S.gh[0][0][0])[e] = 0.0f; (&S.gi[0][0][0])[e] = 0.0f; }
   for (int e = tid; e < FCH * FXP; e += 512) (&S.xin[0][0])[e] = 0.0f;
@@ -102,12 +142,39 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
 
   if (chain) {
     // ================================================================ chain waves
-    f32x2 wT[24];   // W_hh[48q .. 48q+47][k] as pairs for v_pk_fma_f32
+    f32x2 wT[24];   // W_hh[48q .. 48q+47][k] as pairs for v_pk_fma_f32 (K12: see the layout note above)
+    const int c16 = lt & 15;   // K12: lane within the 16-lane DPP row
     {
       const float* Whh = P + L.o[MQ_P_RNN_W_HH];
+      if (kK12) {
+        const int b3 = (c16 >> 3) & 1, b2 = (c16 >> 2) & 1, u0 = 4 * (lt >> 4);
+        const int a0 = u0 + 2 * b3 + b2, a1 = u0 + 2 * b3 + 1 - b2;               // pair A: the units kept
+        const int v0 = u0 + 2 * (1 - b3) + b2, v1 = u0 + 2 * (1 - b3) + 1 - b2;   // pair B: the partner's
 #pragma unroll
-      for (int c = 0; c < 24; ++c) wT[c] = f32x2{Whh[(48 * q + 2 * c) * H + k], Whh[(48 * q + 2 * c + 1) * H + k]};
+        for (int kk = 0; kk < 12; ++kk) {
+          const float* wr = Whh + (12 * c16 + kk) * H;
+          wT[2 * kk] = f32x2{wr[a0], wr[a1]};
+          wT[2 * kk + 1] = f32x2{wr[v0], wr[v1]};
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 24; ++c) wT[c] = f32x2{Whh[(48 * q + 2 * c) * H + k], Whh[(48 * q + 2 * c + 1) * H + k]};
+      }
     }
+    // K12 mat-vec on the 12 dgh values of this lane, reduced to the lane's unit (all four lanes of its quad)
+    auto k12_sum = [&](const f32x4 (&dv)[3]) {
+      f32x2 aA = {0.0f, 0.0f}, aB = {0.0f, 0.0f};
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const f32x2 dd = {dv[m][e], dv[m][e]};
+          aA = pk_fma(wT[2 * (4 * m + e)], dd, aA);
+          aB = pk_fma(wT[2 * (4 * m + e) + 1], dd, aB);
+        }
+      const float x = aA.x + row_ror8(aB.x), y = aA.y + row_ror8(aB.y);
+      return quad_sum(x + row_half_mirror(y));
+    };
     // lane-split inputs of a step: lane q loads gate component q and one of (h_{t-1}, dch, dch, action) at
     // base + idx * stride with per-lane constants, so no lane-dependent branch enters the chain. idx = t except
     // at the edges, clamped with per-lane 0/1 flags: h row 0 stands in for row -1 at t = 0 (hp is zeroed there),
@@ -163,9 +230,35 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       db_h = fmaf(1.0f - m3, mine_h, db_h);
       const float cz = dh * gz;
       if (kStamp) s1 = __builtin_amdgcn_s_memtime();
-      lds_barrier();
+      if (kDec) {
+        group_sync(S.cflag, lt >> 6, lt & 63, Tp - t);
+        if (p == 0) lds_barrier();   // end of chunk t / 16: the producers take it (decoupled roles)
+      } else {
+        lds_barrier();
+      }
       // dh_{t-1} = dh * z + W_hh^T dgh
       const f32x4* dg4 = (const f32x4*)(&S.gh[cb][p][48 * q]);
+      if (kStamp && kK12) {   // K12 with the LDS reads completed before the FMAs (FMA / reduction split not stamped)
+        s2 = __builtin_amdgcn_s_memtime();
+        const f32x4* d12 = (const f32x4*)(&S.gh[cb][p][12 * c16]);
+        f32x4 dv[3] = {d12[0], d12[1], d12[2]};
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        s3 = __builtin_amdgcn_s_memtime();
+        s4 = s3;
+        carry = cz + k12_sum(dv);
+        lookup_w2(nxt);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint64_t s5 = __builtin_amdgcn_s_memtime();
+        ph[0] += s1 - s0; ph[1] += s2 - s1; ph[2] += s3 - s2; ph[3] += s4 - s3; ph[4] += s5 - s4;
+        return;
+      }
+      if (kK12) {
+        const f32x4* d12 = (const f32x4*)(&S.gh[cb][p][12 * c16]);
+        const f32x4 dv[3] = {d12[0], d12[1], d12[2]};
+        carry = cz + k12_sum(dv);
+        if (!kEarlyW2) lookup_w2(nxt);
+        return;
+      }
       if (kStamp) {   // the same arithmetic as below, with the LDS reads completed before the FMAs
         s2 = __builtin_amdgcn_s_memtime();
         f32x4 dv[12];
@@ -275,8 +368,10 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
 #pragma unroll
       for (int i = 0; i < 5; ++i) st[17 + i] = ph[i];
     }
-    lds_barrier();   // producer tail: chunk 0 (2 barriers)
-    lds_barrier();
+    if (!kDec) {
+      lds_barrier();   // producer tail: chunk 0 (2 barriers)
+      lds_barrier();
+    }
     if (q < 3) { slab[o_bi + q * H + k] = db_i; slab[o_bh + q * H + k] = db_h; }
   } else {
     // ================================================================== producer waves
@@ -403,6 +498,40 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     };
     fc2_fetch(Tp - 1);
 
+    if (kDec) {
+      // fc2 grads of chunk c's steps, t descending (the default order): dW2[a][k] += dchosen h_t[k], h_t being the
+      // h_{t-1} record of step t + 1 (the next row of this chunk, or S.hnext for its last step)
+      auto fc2_chunk = [&](int c) {
+        const int cb = c & 1, t0 = FCH * c;
+#pragma unroll
+        for (int p = FCH - 1; p >= 0; --p) {
+          const int t = t0 + p;
+          if (t >= T) continue;
+          const float hn = p < FCH - 1 ? S.gh[cb][p + 1][3 * H + k] : S.hnext[k];
+          const float dchv = w.dch[(int64_t)t * R + r];
+          const int a = *(const int*)(arow + (int64_t)t * d.n);
+          if ((a & 3) == q) {
+            dw2_s[a * H + k] += dchv * hn;
+            if (k == 0) db2_s[a] += dchv;
+          }
+        }
+        if (q == 0) S.hnext[k] = S.gh[cb][0][3 * H + k];   // h_{16c - 1}: read by chunk c - 1's last step
+      };
+      lds_barrier();   // prologue (matches the chain's)
+      issue_rows(cl);
+      for (int c = cl; c >= 0; --c) {
+        lds_barrier();   // the chain has published chunk c; this group has finished chunk c + 1
+        store_rows(c);
+        group_sync(S.pflag, wv, lane, cl + 1 - c);   // chunk c's X1 / XIN rows staged by all producer waves
+        if (c > 0) issue_rows(c - 1);
+        dw_rec(c, 0, 4, false);
+        dw_rec(c, 0, 4, true);
+        dx1_part(c, 0, 12);
+        dx1_epi();
+        dw1_part(0, 4);
+        fc2_chunk(c);
+      }
+    } else {
     lds_barrier();
     for (int c = cl; c >= 0; --c) {
       const int C = c + 1;
@@ -443,6 +572,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     }
     lds_barrier();
     if (!(VAR & 4)) dw1_part(0, 4);
+    }   // !kDec
 
     // per-workgroup slabs in the MFMA C layout: element (16 tile + 4 g + e, 16 tile' + c16)
 #pragma unroll
@@ -495,6 +625,13 @@ inline void launch_bwd_fused(dim3 grid, size_t dyn, hipStream_t s, const Dims& d
     hipLaunchKernelGGL(gru_bwd_fused_kernel<4864>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
   else if (var == 6912)
     hipLaunchKernelGGL(gru_bwd_fused_kernel<6912>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else if (var == 768 + 32768)   // decoupled roles
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 32768>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else if (var == 768 + 32768 + 16384)   // decoupled roles + K12
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 32768 + 16384>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len,
+                       slab1_len);
+  else if (var == 768 + 16384)   // K12 mat-vec layout
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 16384>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
   else if (var == 772)   // diagnostic (wrong gradients): producers idle, the chain alone
     hipLaunchKernelGGL(gru_bwd_fused_kernel<772>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
   else if (var == 1796)  // diagnostic (wrong gradients): SIMD-split chain alone

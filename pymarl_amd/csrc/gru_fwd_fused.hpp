@@ -62,7 +62,11 @@ struct FusedLds {
 // 4 producers idle (recurrence alone on stale gates), 8 per-phase cycle bins, 16 no obs loads, 32 no X1/XIN stores,
 // 64 prologue milestone stamps, 2048 per-phase cycle budget of the chain step (s_memtime stamps of wave 0: LDS reads
 // of h_{t-1} and the input gate | W_hh FMAs | DPP quad reductions | gate math + stores | barrier), summed over the
-// steps into w.slab_mix[16 * block + 8 ..] (diagnostic, scripts/chain_micro.hip).
+// steps into w.slab_mix[16 * block + 8 ..] (diagnostic, scripts/chain_micro.hip), 4096 the K4 mat-vec layout:
+// lane c of 16-lane DPP row r16 sums k in [4c, 4c + 4) for the three gates of the row's four units (the same 48
+// FMAs) and reads one b128 of h_{t-1} instead of four; the twelve partials are reduce-scattered over the row exactly
+// as gru_bwd_fused.hpp's K12 layout does (row_ror:8, row_half_mirror, quad sum, W pairs ordered per lane), leaving
+// the gate sums of unit 4 r16 + 2 b3 + b2 = the lane's quad index, the default gate-math layout.
 // NG: obs gather slots per producer thread (16 * O <= 256 * NG); the host picks the smallest instantiation
 // (launch_fwd_fused) because every slot holds two VGPRs across the whole T loop.
 template <int VAR = 0, int NG = FGATHER>
@@ -156,17 +160,54 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   if (rec) {
     // ================================================================ recurrence waves
     const int j = tid >> 2, q = tid & 3;
-    f32x2 wr[8], wz[8], wn[8];   // W_hh[gate * 64 + j][16 q .. 16 q + 15] as pairs for v_pk_fma_f32
+    constexpr bool kK4 = (VAR & 4096) != 0;
+    const int c16 = tid & 15;   // K4: lane within the 16-lane DPP row
+    f32x2 wr[8], wz[8], wn[8];   // W_hh[gate * 64 + j][16 q .. 16 q + 15] as pairs for v_pk_fma_f32 (K4: see above)
     shared_load();
     {
       const float* Whh = P + L.o[MQ_P_RNN_W_HH];
+      if (kK4) {   // [2 kk] = pair A (units kept), [2 kk + 1] = pair B (the partner's), k = 4 c16 + kk
+        const int b3 = (c16 >> 3) & 1, b2 = (c16 >> 2) & 1, u0 = 4 * (tid >> 4);
+        const int a0 = u0 + 2 * b3 + b2, a1 = u0 + 2 * b3 + 1 - b2;
+        const int v0 = u0 + 2 * (1 - b3) + b2, v1 = u0 + 2 * (1 - b3) + 1 - b2;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        wr[k] = f32x2{Whh[(0 * H + j) * H + 16 * q + 2 * k], Whh[(0 * H + j) * H + 16 * q + 2 * k + 1]};
-        wz[k] = f32x2{Whh[(1 * H + j) * H + 16 * q + 2 * k], Whh[(1 * H + j) * H + 16 * q + 2 * k + 1]};
-        wn[k] = f32x2{Whh[(2 * H + j) * H + 16 * q + 2 * k], Whh[(2 * H + j) * H + 16 * q + 2 * k + 1]};
+        for (int kk = 0; kk < 4; ++kk) {
+          const int k = 4 * c16 + kk;
+          wr[2 * kk] = f32x2{Whh[(0 * H + a0) * H + k], Whh[(0 * H + a1) * H + k]};
+          wr[2 * kk + 1] = f32x2{Whh[(0 * H + v0) * H + k], Whh[(0 * H + v1) * H + k]};
+          wz[2 * kk] = f32x2{Whh[(1 * H + a0) * H + k], Whh[(1 * H + a1) * H + k]};
+          wz[2 * kk + 1] = f32x2{Whh[(1 * H + v0) * H + k], Whh[(1 * H + v1) * H + k]};
+          wn[2 * kk] = f32x2{Whh[(2 * H + a0) * H + k], Whh[(2 * H + a1) * H + k]};
+          wn[2 * kk + 1] = f32x2{Whh[(2 * H + v0) * H + k], Whh[(2 * H + v1) * H + k]};
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          wr[k] = f32x2{Whh[(0 * H + j) * H + 16 * q + 2 * k], Whh[(0 * H + j) * H + 16 * q + 2 * k + 1]};
+          wz[k] = f32x2{Whh[(1 * H + j) * H + 16 * q + 2 * k], Whh[(1 * H + j) * H + 16 * q + 2 * k + 1]};
+          wn[k] = f32x2{Whh[(2 * H + j) * H + 16 * q + 2 * k], Whh[(2 * H + j) * H + 16 * q + 2 * k + 1]};
+        }
       }
     }
+    // K4 mat-vec: 4 h values -> this lane's unit's three gate sums (every lane of the quad)
+    auto k4_sums = [&](const f32x4 hv, float& sr, float& sz, float& sn) {
+      f32x2 rA = {0.0f, 0.0f}, rB = {0.0f, 0.0f}, zA = {0.0f, 0.0f}, zB = {0.0f, 0.0f}, nA = {0.0f, 0.0f},
+            nB = {0.0f, 0.0f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const f32x2 hh = {hv[kk], hv[kk]};
+        rA = pk_fma(wr[2 * kk], hh, rA); rB = pk_fma(wr[2 * kk + 1], hh, rB);
+        zA = pk_fma(wz[2 * kk], hh, zA); zB = pk_fma(wz[2 * kk + 1], hh, zB);
+        nA = pk_fma(wn[2 * kk], hh, nA); nB = pk_fma(wn[2 * kk + 1], hh, nB);
+      }
+      auto red = [](f32x2 a, f32x2 b) {
+        const float x = a.x + row_ror8(b.x), y = a.y + row_ror8(b.y);
+        return quad_sum(x + row_half_mirror(y));
+      };
+      sr = red(rA, rB);
+      sz = red(zA, zB);
+      sn = red(nA, nB);
+    };
     const float bhr = P[L.o[MQ_P_RNN_B_HH] + j], bhz = P[L.o[MQ_P_RNN_B_HH] + H + j],
                 bhn = P[L.o[MQ_P_RNN_B_HH] + 2 * H + j];
     shared_store();
@@ -188,7 +229,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       if (VAR & 2048) s0 = __builtin_amdgcn_s_memtime();
       const float own = S.gi[c & 1][p][gcol];   // issued with the h reads below (same LDS latency window)
       float sr, sz, sn;
-      if (VAR & 2048) {   // the same arithmetic with the LDS reads completed first
+      if (kK4) {
+        const f32x4 hv = *(const f32x4*)(&hb[4 * c16]);
+        if (VAR & 2048) {
+          asm volatile("s_waitcnt lgkmcnt(0)" :: "v"(own), "v"(hv) : "memory");
+          s1 = __builtin_amdgcn_s_memtime();
+          s2 = s1;
+        }
+        k4_sums(hv, sr, sz, sn);
+        if (VAR & 2048) {
+          asm volatile("" :: "v"(sr), "v"(sz), "v"(sn));
+          s3 = __builtin_amdgcn_s_memtime();
+        }
+      } else if (VAR & 2048) {   // the same arithmetic with the LDS reads completed first
         const f32x4* hv4 = (const f32x4*)(&hb[16 * q]);
         f32x4 hv[4];
 #pragma unroll
@@ -529,7 +582,8 @@ inline void launch_fwd_fused_v(dim3 grid, hipStream_t s, const Dims& d, const Re
 inline void launch_fwd_fused(dim3 grid, hipStream_t s, const Dims& d, const Rep& rp, const float* P0, const float* P1,
                              const Lay& L, const Work& w) {
   static const int var = [] { const char* e = std::getenv("MQ_FWD_VAR"); return e ? std::atoi(e) : 0; }();
-  if (var == 256) launch_fwd_fused_v<256>(grid, s, d, rp, P0, P1, L, w);
+  if (var == 4096) launch_fwd_fused_v<4096>(grid, s, d, rp, P0, P1, L, w);   // K4 mat-vec layout
+  else if (var == 256) launch_fwd_fused_v<256>(grid, s, d, rp, P0, P1, L, w);
   else if (var == 512) launch_fwd_fused_v<512>(grid, s, d, rp, P0, P1, L, w);
   else if (var == 128) launch_fwd_fused_v<128>(grid, s, d, rp, P0, P1, L, w);  // no chain priority
   else launch_fwd_fused_v<0>(grid, s, d, rp, P0, P1, L, w);

@@ -3,6 +3,7 @@
 // forward, 8192 in the BPTT; each the production schedule with the chain's LDS reads completed before its FMAs).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 scripts/chain_micro.hip -o scripts/chain_micro && scripts/chain_micro
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -97,6 +98,25 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL((gru_fwd_fused_kernel<2052, 5>), dim3(d.R, 2), dim3(512), 0, 0, d, rp, (const float*)P0, (const float*)P1, L, w);
   CK(hipDeviceSynchronize());
   fwd_budget("producers idle");
+  {  // K4 mat-vec layout: time, budget, and its outputs against production's
+    const int64_t nq = 2 * RT * A, nh = RT * 64;
+    std::vector<float> q0(nq), q1(nq), h0(nh), h1(nh);
+    hipLaunchKernelGGL((gru_fwd_fused_kernel<0, 5>), dim3(d.R, 2), dim3(512), 0, 0, d, rp, (const float*)P0, (const float*)P1, L, w);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(q0.data(), w.Q, nq * 4, hipMemcpyDeviceToHost)); CK(hipMemcpy(h0.data(), w.Hs, nh * 4, hipMemcpyDeviceToHost));
+    hipLaunchKernelGGL((gru_fwd_fused_kernel<4096, 5>), dim3(d.R, 2), dim3(512), 0, 0, d, rp, (const float*)P0, (const float*)P1, L, w);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(q1.data(), w.Q, nq * 4, hipMemcpyDeviceToHost)); CK(hipMemcpy(h1.data(), w.Hs, nh * 4, hipMemcpyDeviceToHost));
+    double mq = 0, dq = 0, dh = 0;
+    for (int64_t i = 0; i < nq; ++i) { mq = std::max(mq, (double)fabsf(q0[i])); dq = std::max(dq, (double)fabsf(q0[i] - q1[i])); }
+    for (int64_t i = 0; i < nh; ++i) dh = std::max(dh, (double)fabsf(h0[i] - h1[i]));
+    printf("K4 vs production: max |dQ| %.3e (of max |Q| %.3e), max |dh| %.3e\n", dq, mq, dh);
+    printf("fused fwd K4 %.1f us | production %.1f us | K4 producers idle %.1f us\n", runf(gru_fwd_fused_kernel<4096, 5>),
+           runf(gru_fwd_fused_kernel<0, 5>), runf(gru_fwd_fused_kernel<4100, 5>));
+    hipLaunchKernelGGL((gru_fwd_fused_kernel<4096 + 2048, 5>), dim3(d.R, 2), dim3(512), 0, 0, d, rp, (const float*)P0, (const float*)P1, L, w);
+    CK(hipDeviceSynchronize());
+    fwd_budget("K4 (lds | - | fmas+reduction | gates | barrier)");
+  }
 
   const size_t dyn = (2 * A * 64 + A) * 4;
   auto runb = [&](auto kern) {
@@ -124,6 +144,45 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 8192>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
   CK(hipDeviceSynchronize());
   bwd_budget("production");
+  // K12 mat-vec layout: time, phase budget, and its slabs against production's (same inputs; rounding only)
+  {
+    auto slabs = [&]() {
+      std::vector<float> a((size_t)d.R * len_rnn), b((size_t)d.R * len1);
+      CK(hipMemcpy(a.data(), w.slab_rnn, a.size() * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(b.data(), w.slab_fc1, b.size() * 4, hipMemcpyDeviceToHost));
+      a.insert(a.end(), b.begin(), b.end());
+      return a;
+    };
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+    CK(hipDeviceSynchronize());
+    const std::vector<float> ref = slabs();
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 16384>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+    CK(hipDeviceSynchronize());
+    const std::vector<float> got = slabs();
+    double mx = 0, md = 0;
+    for (size_t i = 0; i < ref.size(); ++i) { mx = std::max(mx, (double)fabsf(ref[i])); md = std::max(md, (double)fabsf(ref[i] - got[i])); }
+    printf("K12 vs production slabs: max |diff| %.3e of max |ref| %.3e (rel %.2e)\n", md, mx, md / mx);
+    printf("fused bwd K12 %.1f us | production %.1f us | K12 stamped %.1f us\n",
+           runb(gru_bwd_fused_kernel<768 + 16384>), runb(gru_bwd_fused_kernel<768>),
+           runb(gru_bwd_fused_kernel<768 + 16384 + 8192>));
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 16384 + 8192>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+    CK(hipDeviceSynchronize());
+    bwd_budget("K12 (fmas+reduction in the last bin)");
+    printf("fused bwd K12 producers idle %.1f us\n", runb(gru_bwd_fused_kernel<772 + 16384>));
+    // decoupled roles: bitwise production, and its time
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 32768>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+    CK(hipDeviceSynchronize());
+    const std::vector<float> dec = slabs();
+    size_t ndiff = 0;
+    for (size_t i = 0; i < ref.size(); ++i) ndiff += ref[i] != dec[i];
+    printf("decoupled vs production slabs: %zu of %zu differ\n", ndiff, ref.size());
+    printf("fused bwd decoupled %.1f us | decoupled+K12 %.1f us | production %.1f us\n",
+           runb(gru_bwd_fused_kernel<768 + 32768>), runb(gru_bwd_fused_kernel<768 + 32768 + 16384>),
+           runb(gru_bwd_fused_kernel<768>));
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 32768 + 8192>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+    CK(hipDeviceSynchronize());
+    bwd_budget("decoupled (barrier bin = chain group sync)");
+  }
   hipLaunchKernelGGL(gru_bwd_fused_kernel<772 + 8192>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
   CK(hipDeviceSynchronize());
   bwd_budget("producers idle");
