@@ -524,6 +524,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
         store_rows(c);
         group_sync(S.pflag, wv, lane, cl + 1 - c);   // chunk c's X1 / XIN rows staged by all producer waves
         if (c > 0) issue_rows(c - 1);
+        if (VAR & 4) continue;   // diagnostic: producers idle
         dw_rec(c, 0, 4, false);
         dw_rec(c, 0, 4, true);
         dx1_part(c, 0, 12);

@@ -34,6 +34,70 @@ float* dev_rand(size_t n, float scale) {
   return d;
 }
 
+// Prototype: the whole BPTT dh chain of one row in ONE wave (lane j = unit j): W_hh columns in VGPRs (96 pairs), the
+// 192 dgh values of a step broadcast from LDS (48 ds_read_b128, all lanes one address), no cross-wave sync at all.
+// Writes the same [dgh | h_{t-1}] / dgi history rows as the production chain (into a chunk ring in LDS) so the LDS
+// traffic is representative; NACC independent accumulator pairs in the mat-vec.
+template <int NACC>
+__global__ __launch_bounds__(512) void w1_chain_proto(Dims d, const float* __restrict__ P, Lay L, Work w,
+                                                      const int64_t* __restrict__ acts, float* __restrict__ out) {
+  __shared__ float gh[2][FCH][BRP], gi[2][FCH][BRP];
+  __shared__ float w2s[16 * H];
+  const int tid = threadIdx.x, r = blockIdx.x, R = d.R, T = d.T, Tp = d.Tp;
+  for (int i = tid; i < d.A * H; i += 512) w2s[i] = P[L.o[MQ_P_FC2_W] + i];
+  __syncthreads();
+  if (tid >= 64) return;
+  const int j = tid;
+  f32x2 wp[96];
+  const float* Whh = P + L.o[MQ_P_RNN_W_HH];
+#pragma unroll
+  for (int i = 0; i < 96; ++i) wp[i] = f32x2{Whh[(2 * i) * H + j], Whh[(2 * i + 1) * H + j]};
+  struct In { float gr, gz, gn, ghn, hp, dch; int a; };
+  auto load = [&](int t, In& s) {
+    const int tc = max(t, 0);
+    const float* g = w.Gates + ((int64_t)tc * R + r) * (4 * H) + j;
+    s.gr = g[0]; s.gz = g[H]; s.gn = g[2 * H]; s.ghn = g[3 * H];
+    s.hp = w.Hs[((int64_t)max(tc - 1, 0) * R + r) * H + j];
+    s.dch = w.dch[(int64_t)min(tc, T - 1) * R + r];
+    s.a = (int)acts[(int64_t)tc * R + r];
+  };
+  In sa, sb, sc;
+  load(Tp - 1, sa); load(Tp - 2, sb);
+  float carry = 0.0f, dbs = 0.0f;
+  auto step = [&](int t, const In& cur, In& ahead) {
+    load(t - 2, ahead);
+    const int p = t & (FCH - 1), cb = (t / FCH) & 1;
+    const float hp = t > 0 ? cur.hp : 0.0f, dchv = t < T ? cur.dch : 0.0f;
+    const float dh = carry + dchv * w2s[cur.a * H + j];
+    const float dn = dh * (1.0f - cur.gz), dz = dh * (hp - cur.gn);
+    const float dan = dn * (1.0f - cur.gn * cur.gn);
+    const float dar = (dan * cur.ghn) * (cur.gr * (1.0f - cur.gr));
+    const float daz = dz * (cur.gz * (1.0f - cur.gz));
+    gh[cb][p][j] = dar; gh[cb][p][H + j] = daz; gh[cb][p][2 * H + j] = dan * cur.gr; gh[cb][p][3 * H + j] = hp;
+    gi[cb][p][j] = dar; gi[cb][p][H + j] = daz; gi[cb][p][2 * H + j] = dan;
+    dbs += dar + daz + dan;
+    const f32x4* dg4 = (const f32x4*)&gh[cb][p][0];
+    f32x2 acc[NACC];
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) acc[i] = f32x2{0.0f, 0.0f};
+#pragma unroll
+    for (int c4 = 0; c4 < 48; ++c4) {
+      const f32x4 v = dg4[c4];
+      acc[(2 * c4) % NACC] = pk_fma(wp[2 * c4], f32x2{v[0], v[1]}, acc[(2 * c4) % NACC]);
+      acc[(2 * c4 + 1) % NACC] = pk_fma(wp[2 * c4 + 1], f32x2{v[2], v[3]}, acc[(2 * c4 + 1) % NACC]);
+    }
+    float sum = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) sum += acc[i].x + acc[i].y;
+    carry = dh * cur.gz + sum;
+  };
+  int t = Tp - 1;
+  for (; t - 2 >= 0; t -= 3) { step(t, sa, sc); step(t - 1, sb, sa); step(t - 2, sc, sb); }
+  if (t >= 0) step(t, sa, sc);
+  if (t - 1 >= 0) step(t - 1, sb, sa);
+  out[(int64_t)r * H + j] = carry + dbs;
+}
+
 int main(int argc, char** argv) {
   int B = argc > 1 ? atoi(argv[1]) : 32, n = argc > 2 ? atoi(argv[2]) : 8, T = argc > 3 ? atoi(argv[3]) : 120;
   const int A = 14, O = 80;
@@ -182,6 +246,33 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 32768 + 8192>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
     CK(hipDeviceSynchronize());
     bwd_budget("decoupled (barrier bin = chain group sync)");
+    // SIMD-split roles (chain waves 0, 1, 4, 5 on SIMDs 0 / 1; producers on 2 / 3) with decoupled syncs
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 32768 + 1024>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+    CK(hipDeviceSynchronize());
+    const std::vector<float> spl = slabs();
+    ndiff = 0;
+    for (size_t i = 0; i < ref.size(); ++i) ndiff += ref[i] != spl[i];
+    printf("split+decoupled vs production slabs: %zu of %zu differ\n", ndiff, ref.size());
+    printf("fused bwd split+decoupled %.1f us | split+decoupled+K12 %.1f us | decoupled+prio %.1f us | split+dec idle %.1f us\n",
+           runb(gru_bwd_fused_kernel<768 + 32768 + 1024>), runb(gru_bwd_fused_kernel<768 + 32768 + 1024 + 16384>),
+           runb(gru_bwd_fused_kernel<768 + 32768 + 128>), runb(gru_bwd_fused_kernel<772 + 32768 + 1024>));
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 32768 + 1024 + 8192>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+    CK(hipDeviceSynchronize());
+    bwd_budget("split+decoupled");
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 32768 + 1024 + 8192 + 16384>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+    CK(hipDeviceSynchronize());
+    bwd_budget("split+decoupled+K12");
+  }
+  {  // one-wave chain prototype (timing only)
+    std::vector<int64_t> ta((int64_t)(T + 1) * d.R);
+    for (auto& a : ta) a = rand() % A;
+    int64_t* dta; CK(hipMalloc(&dta, ta.size() * 8)); CK(hipMemcpy(dta, ta.data(), ta.size() * 8, hipMemcpyHostToDevice));
+    float* o1; CK(hipMalloc(&o1, (int64_t)d.R * 64 * 4));
+    auto runp = [&](auto kern) {
+      return time_med([&] { hipLaunchKernelGGL(kern, dim3(d.R), dim3(512), 0, 0, d, (const float*)P0, L, w, (const int64_t*)dta, o1); });
+    };
+    printf("one-wave chain prototype: NACC 2 %.1f us | 4 %.1f us | 8 %.1f us\n", runp(w1_chain_proto<2>),
+           runp(w1_chain_proto<4>), runp(w1_chain_proto<8>));
   }
   hipLaunchKernelGGL(gru_bwd_fused_kernel<772 + 8192>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
   CK(hipDeviceSynchronize());
