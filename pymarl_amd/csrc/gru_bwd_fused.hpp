@@ -56,7 +56,7 @@ MQ_DEV void group_sync(volatile int* flags, int wave_in_group, int lane, int cnt
 
 inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_fwd_ok(I, O, A, n, RT); }
 
-// VAR: ablation bits (production = 0): 4 producers do no MFMA work, 8 per-phase cycle bins of the chain
+// VAR: ablation bits (production: see launch_bwd_fused): 4 producers do no MFMA work, 8 per-phase cycle bins of the chain
 // (scripts/rec_micro.hip), 128 chain waves at s_setprio 2, 256 the chain's inputs loaded two steps ahead,
 // 512 the X1 / XIN rows of the next chunk loaded one chunk ahead, 1024 SIMD-split roles: the chain runs in waves
 // 0, 1, 4, 5 and the producers in waves 2, 3, 6, 7. Waves w and w + 4 of a 512-thread workgroup share a SIMD, so
@@ -66,7 +66,16 @@ inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_
 // accumulator pairs in the W_hh^T mat-vec, 8192 per-phase cycle budget of the chain step (s_memtime stamps of chain
 // wave 0: inputs + gate math + LDS stores | barrier | LDS reads of dgh | W_hh^T FMAs | DPP quad reduction + W2
 // lookup), summed over the steps into w.slab_mix[32 * block + 17 ..] (diagnostic, scripts/chain_micro.hip), 16384
-// the K12 mat-vec layout (below), 32768 decoupled roles (below).
+// the K12 mat-vec layout (below), 32768 decoupled roles (below), 65536 the linearised step (below).
+//
+// Linearised step (VAR 65536). Every gate derivative of a step is dh times a coefficient of that step's inputs:
+// dn = dh (1 - z), dz = dh (h_{t-1} - n), d(a_n) = dh (1 - z)(1 - n^2), d(a_r) = d(a_n) ghn r (1 - r),
+// d(a_z) = dh (h_{t-1} - n) z (1 - z). So each lane's record value is dh * c (+ h_{t-1} in the h slot) and the
+// carry's own term is dh * z, with c computed from the gate record before dh is known: during the previous step,
+// beside its mat-vec. What stays on the dh chain is dh = carry + dchosen W2[a], two products, the record stores and
+// the mat-vec (the default puts ~15 dependent VALU / DPP operations there: 350 of 1,050 cycles a step measured
+// with the producers idle). Inputs are loaded three steps ahead (four slots). The products are associated
+// differently from the default, so results differ from it by rounding.
 //
 // Decoupled roles (VAR 32768). Default: every chain step ends in an s_barrier of all eight waves, so the chain waits
 // for the producer waves whenever a producer phase runs long (measured at cfg2: the barrier is 334 of 1,420 cycles a
@@ -97,6 +106,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
   constexpr bool kStamp = (VAR & 8192) != 0;
   constexpr bool kK12 = (VAR & 16384) != 0;
   constexpr bool kDec = (VAR & 32768) != 0;
+  constexpr bool kLin = (VAR & 65536) != 0;
   const bool chain = kSplit ? ((tid >> 7) & 1) == 0 : tid < 256;
   // role-local thread id 0..255 (wave-uniform role; lanes of a quad stay in one wave)
   const int lt = kSplit ? ((tid & 127) | ((tid >> 8) << 7)) : (tid & 255), k = lt >> 2, q = lt & 3;
@@ -181,7 +191,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     // dch row T-1 for row T at t = T (dchv is zeroed there). The action is read as the low word of the int64
     // (little-endian, 0 <= a < A). w2 = W2[a_t][k] is looked up one step ahead (end of the previous step), off
     // the dh chain.
-    struct In { float g, aux, w2; };
+    struct In { float g, aux, w2, wd, ci, ch, hq, gz; };   // kLin: wd .. gz are the step's coefficients
     const float* aux_base;
     int64_t aux_stride;
     if (q == 0) { aux_base = w.Hs + (int64_t)r * H + k - (int64_t)R * H; aux_stride = (int64_t)R * H; }
@@ -190,7 +200,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     const float* g_base = w.Gates + (int64_t)r * (4 * H) + q * H + k;
     const int e0 = q == 0 ? 1 : 0, e12 = (q == 1 || q == 2) ? 1 : 0;
     auto load = [&](int t, In& s) {
-      const int tc = max(t, 0);
+      const int tc = (VAR & 131072) ? T : max(t, 0);   // VAR 131072, diagnostic only: every step loads step T
       const int idx = tc + (e0 & (tc == 0 ? 1 : 0)) - (e12 & (tc >= T ? 1 : 0));
       s.g = g_base[(int64_t)tc * R * (4 * H)];
       s.aux = aux_base[idx * aux_stride];
@@ -305,7 +315,79 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       }
       if (!kEarlyW2) lookup_w2(nxt);
     };
+    // kLin: the step's coefficients (see the note above), computed one step ahead
+    auto coeffs = [&](int t, In& s) {
+      const float gr = quad_bcast<0>(s.g), gz = quad_bcast<1>(s.g), gn = quad_bcast<2>(s.g), ghn = quad_bcast<3>(s.g);
+      const float hp = t > 0 ? quad_bcast<0>(s.aux) : 0.0f;
+      const float dchv = t < T ? quad_bcast<2>(s.aux) : 0.0f;
+      const float an = (1.0f - gz) * (1.0f - gn * gn);
+      const float ar = (an * ghn) * (gr * (1.0f - gr));
+      const float az = (hp - gn) * (gz * (1.0f - gz));
+      const float rzc = fmaf(m0, ar, m1 * az);
+      s.ci = fmaf(m2 + m3, an, rzc);       // dgi component q (q = 3: the unused slot)
+      s.ch = fmaf(m2, an * gr, rzc);       // dgh component q (q = 3: 0, the slot holds h_{t-1})
+      s.hq = m3 * hp;
+      s.wd = dchv * s.w2;
+      s.gz = gz;
+    };
+    auto lstep = [&](int t, const In& cur, In& nxt, In& ahead) {
+      load(t - 3, ahead);
+      const int p = t & (FCH - 1), cb = (t / FCH) & 1;
+      const float dh = carry + cur.wd;
+      const float mine_i = dh * cur.ci;
+      const float mine_h = fmaf(dh, cur.ch, cur.hq);
+      S.gh[cb][p][q * H + k] = mine_h;
+      S.gi[cb][p][q * H + k] = mine_i;
+      db_i = fmaf(1.0f - m3, mine_i, db_i);
+      db_h = fmaf(1.0f - m3, mine_h, db_h);
+      if (kDec) {
+        group_sync(S.cflag, lt >> 6, lt & 63, Tp - t);
+        if (p == 0) lds_barrier();
+      } else {
+        lds_barrier();
+      }
+      float part;
+      if (kK12) {
+        const f32x4* d12 = (const f32x4*)(&S.gh[cb][p][12 * c16]);
+        const f32x4 dv[3] = {d12[0], d12[1], d12[2]};
+        lookup_w2(nxt);   // the next step's W2[a][k] and coefficients, beside this step's LDS reads and FMAs
+        coeffs(t - 1, nxt);
+        carry = fmaf(dh, cur.gz, k12_sum(dv));
+        return;
+      }
+      const f32x4* dg4 = (const f32x4*)(&S.gh[cb][p][48 * q]);
+      f32x2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
+#pragma unroll
+      for (int c4 = 0; c4 < 12; ++c4) {
+        const f32x4 dg = dg4[c4];
+        a01 = pk_fma(wT[2 * c4], f32x2{dg[0], dg[1]}, a01);
+        a23 = pk_fma(wT[2 * c4 + 1], f32x2{dg[2], dg[3]}, a23);
+      }
+      lookup_w2(nxt);
+      coeffs(t - 1, nxt);
+      part = (a01.x + a01.y) + (a23.x + a23.y);
+      carry = fmaf(dh, cur.gz, quad_sum(part));
+    };
     In sa, sb, sc, sd;
+    if (kLin) {
+      load(Tp - 1, sa);
+      load(Tp - 2, sb);
+      load(Tp - 3, sc);
+      drain_vmem();
+      lds_barrier();
+      lookup_w2(sa);
+      coeffs(Tp - 1, sa);
+      int t = Tp - 1;
+      for (; t - 3 >= 0; t -= 4) {
+        lstep(t, sa, sb, sd);
+        lstep(t - 1, sb, sc, sa);
+        lstep(t - 2, sc, sd, sb);
+        lstep(t - 3, sd, sa, sc);
+      }
+      if (t >= 0) lstep(t, sa, sb, sd);
+      if (t - 1 >= 0) lstep(t - 1, sb, sc, sa);
+      if (t - 2 >= 0) lstep(t - 2, sc, sd, sb);
+    } else {
     load(Tp - 1, sa);
     if (VAR & (256 | 2048)) load(Tp - 2, sb);
     if (kEarlyW2) load(Tp - 3, sc);
@@ -362,6 +444,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       }
       if (t >= 0) step(t, sa, sb, sb, 1);
     }
+    }   // !kLin
     if (VAR & 128) __builtin_amdgcn_s_setprio(0);
     if (kStamp && tid == 0) {
       uint64_t* st = (uint64_t*)w.slab_mix + 32 * blockIdx.x;
@@ -604,12 +687,14 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
         (S.db1[0][tid] + S.db1[1][tid]) + (S.db1[2][tid] + S.db1[3][tid]);
 }
 
-// Host: production is VAR 768 = 256 (chain inputs two steps ahead: -2.5 us in the cfg2 pipeline, r01k A/B) + 512
-// (X1 / XIN rows one chunk ahead: -0.7 us); MQ_BWD_VAR
-// selects another variant for in-pipeline A/B runs.
+// Host: production is VAR 82688 = 512 (X1 / XIN rows one chunk ahead: -0.7 us, r01k A/B) + 256 (unused by the
+// linearised step, which loads its inputs three steps ahead) + 65536 (linearised step) + 16384 (K12 mat-vec):
+// -3.5 us a BPTT against VAR 768 (chain micro 88.8 -> 84.9 us; cfg2 pipeline 0.2277 -> 0.2250 ms a step, r03
+// A/B: profiles/r03_ab_lin_k12.json, teacher-forced parity green at it). MQ_BWD_VAR selects another variant for
+// in-pipeline A/B runs.
 inline void launch_bwd_fused(dim3 grid, size_t dyn, hipStream_t s, const Dims& d, const Rep& rp, const float* P,
                              const Lay& L, const Work& w, int64_t slab_len, int64_t slab1_len) {
-  static const int var = [] { const char* e = std::getenv("MQ_BWD_VAR"); return e ? std::atoi(e) : 768; }();
+  static const int var = [] { const char* e = std::getenv("MQ_BWD_VAR"); return e ? std::atoi(e) : 768 + 65536 + 16384; }();
   if (var == 256)
     hipLaunchKernelGGL(gru_bwd_fused_kernel<256>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
   else if (var == 128)
@@ -630,6 +715,11 @@ inline void launch_bwd_fused(dim3 grid, size_t dyn, hipStream_t s, const Dims& d
     hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 32768>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
   else if (var == 768 + 32768 + 16384)   // decoupled roles + K12
     hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 32768 + 16384>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len,
+                       slab1_len);
+  else if (var == 768 + 65536)   // linearised step
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 65536>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else if (var == 768 + 65536 + 16384)   // linearised step + K12
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 65536 + 16384>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len,
                        slab1_len);
   else if (var == 768 + 16384)   // K12 mat-vec layout
     hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 16384>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);

@@ -7,7 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
-#include "../pymarl_amd/csrc/gru_bwd_fused.hpp"
+#include "gru_bwd_w1.hpp"
 using namespace mq;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
@@ -208,6 +208,40 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 8192>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
   CK(hipDeviceSynchronize());
   bwd_budget("production");
+  {  // linearised step (VAR 65536): slabs vs production (rounding) and time
+    auto slabs = [&]() {
+      std::vector<float> a((size_t)d.R * len_rnn), b((size_t)d.R * len1);
+      CK(hipMemcpy(a.data(), w.slab_rnn, a.size() * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(b.data(), w.slab_fc1, b.size() * 4, hipMemcpyDeviceToHost));
+      a.insert(a.end(), b.begin(), b.end());
+      return a;
+    };
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+    CK(hipDeviceSynchronize());
+    const std::vector<float> ref = slabs();
+    for (int v : {65536, 65536 + 16384}) {
+      if (v == 65536)
+        hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 65536>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+      else
+        hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 65536 + 16384>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+      CK(hipDeviceSynchronize());
+      const std::vector<float> got = slabs();
+      double mx = 0, md = 0;
+      for (size_t i = 0; i < ref.size(); ++i) { mx = std::max(mx, (double)fabsf(ref[i])); md = std::max(md, (double)fabsf(ref[i] - got[i])); }
+      printf("linearised%s vs production slabs: max |diff| %.3e of max |ref| %.3e (rel %.2e)\n", v == 65536 ? "" : "+K12", md, mx, md / mx);
+    }
+    printf("fused bwd linearised %.1f us | linearised+K12 %.1f us | production %.1f us\n",
+           runb(gru_bwd_fused_kernel<768 + 65536>), runb(gru_bwd_fused_kernel<768 + 65536 + 16384>),
+           runb(gru_bwd_fused_kernel<768>));
+    printf("fused bwd producers idle: linearised %.1f us | linearised+K12 %.1f us | production %.1f us\n",
+           runb(gru_bwd_fused_kernel<772 + 65536>), runb(gru_bwd_fused_kernel<772 + 65536 + 16384>),
+           runb(gru_bwd_fused_kernel<772>));
+  }
+  // diagnostic: the chain's global loads all hit one cache-resident step (results meaningless)
+  printf("fused bwd fixed-address loads: linearised+K12 %.1f us | idle %.1f us | production %.1f us | idle %.1f us\n",
+         runb(gru_bwd_fused_kernel<768 + 65536 + 16384 + 131072>), runb(gru_bwd_fused_kernel<772 + 65536 + 16384 + 131072>),
+         runb(gru_bwd_fused_kernel<768 + 131072>), runb(gru_bwd_fused_kernel<772 + 131072>));
+  if (argc > 4 && atoi(argv[4]) == 0) return 0;   // only the production and linearised sections
   // K12 mat-vec layout: time, phase budget, and its slabs against production's (same inputs; rounding only)
   {
     auto slabs = [&]() {
@@ -262,6 +296,34 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 32768 + 1024 + 8192 + 16384>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
     CK(hipDeviceSynchronize());
     bwd_budget("split+decoupled+K12");
+  }
+  {  // the one-wave-chain BPTT kernel: slabs vs production (rounding) and time
+    const size_t dyn = (2 * A * 64 + A) * 4;
+    auto slabs = [&]() {
+      std::vector<float> a((size_t)d.R * len_rnn), b((size_t)d.R * len1);
+      CK(hipMemcpy(a.data(), w.slab_rnn, a.size() * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(b.data(), w.slab_fc1, b.size() * 4, hipMemcpyDeviceToHost));
+      a.insert(a.end(), b.begin(), b.end());
+      return a;
+    };
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+    CK(hipDeviceSynchronize());
+    const std::vector<float> ref = slabs();
+    hipLaunchKernelGGL(gru_bwd_w1_kernel<0>, dim3(d.R), dim3(512), dyn, 0, d, rp, (const float*)P0, L, w, len_rnn, len1);
+    CK(hipDeviceSynchronize());
+    const std::vector<float> got = slabs();
+    // per region: w_ih, w_hh, b_ih, b_hh, fc2.w, fc2.b of every row slab, then fc1 slabs
+    double mx = 0, md = 0;
+    size_t worst = 0;
+    for (size_t i = 0; i < ref.size(); ++i) {
+      mx = std::max(mx, (double)fabsf(ref[i]));
+      const double dd = fabs((double)ref[i] - got[i]);
+      if (dd > md) { md = dd; worst = i; }
+    }
+    printf("W1 vs production slabs: max |diff| %.3e of max |ref| %.3e (rel %.2e) at %zu (ref %.6e got %.6e)\n", md, mx,
+           md / mx, worst, ref[worst], got[worst]);
+    printf("fused bwd W1 %.1f us | production %.1f us\n",
+           runb(gru_bwd_w1_kernel<0>), runb(gru_bwd_fused_kernel<768>));
   }
   {  // one-wave chain prototype (timing only)
     std::vector<int64_t> ta((int64_t)(T + 1) * d.R);
