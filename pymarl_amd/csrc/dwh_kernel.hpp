@@ -29,7 +29,7 @@ constexpr int DWH_T = 32;   // output tile edge
 
 // grid = ceil(NH / 32) * ceil((S + 1) / 32) * nsplit (tiles_j = ceil(NH / 32)), 256 threads.
 // VAR (scripts/rec_micro.hip only): 1 no MFMA, 2 no operand loads. U: MFMAs (2 m-rows each) per pipelined block.
-template <int VAR, int U>
+template <int VAR, int U, int NB = 2>
 MQ_DEV void dwh_body(Dims d, Lay L, const float* __restrict__ dHYP, const float* __restrict__ S0,
                      float* __restrict__ slab, int64_t len, int nsplit, int tiles_j, int lin) {
   __shared__ float red[4][DWH_T * (DWH_T + 1)];
@@ -48,7 +48,10 @@ MQ_DEV void dwh_body(Dims d, Lay L, const float* __restrict__ dHYP, const float*
   const float amul = s < S ? 1.0f : 0.0f, aadd = s == S ? 1.0f : 0.0f;
 
   f32x16 acc = {};
-  float a0[U], b0[U], a1[U], b1[U];   // two register buffers (static indices only)
+  // NB register buffers of U MFMA steps each (static indices only): block k + NB - 1 is fetched while block k's
+  // MFMAs run, so NB - 1 blocks of loads are in flight. Each block costs ~one memory latency when NB = 2 (8 MFMAs
+  // are ~0.2 us, a load round trip 1 - 2 us under the reduction's traffic): the m loop was latency-bound.
+  float a[NB][U], b[NB][U];
   auto load = [&](float (&a)[U], float (&b)[U], int st0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -72,16 +75,18 @@ MQ_DEV void dwh_body(Dims d, Lay L, const float* __restrict__ dHYP, const float*
     }
   };
   constexpr int BLK = 4 * U;   // steps per block over the four waves
-  int st = sb + wv;
+  const int st = sb + wv;
   const int nblk = (se - sb + BLK - 1) / BLK;
-  if (nblk > 0) load(a0, b0, st);
-  for (int blk = 0; blk < nblk; blk += 2) {
-    if (blk + 1 < nblk) load(a1, b1, st + BLK);
-    mma(a0, b0);
-    if (blk + 1 >= nblk) break;
-    if (blk + 2 < nblk) load(a0, b0, st + 2 * BLK);
-    mma(a1, b1);
-    st += 2 * BLK;
+#pragma unroll
+  for (int p = 0; p < NB - 1; ++p)
+    if (p < nblk) load(a[p], b[p], st + p * BLK);
+  for (int blk = 0; blk < nblk; blk += NB) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {   // block blk + q sits in buffer q; block blk + q + NB - 1 goes to buffer q - 1
+      if (blk + q >= nblk) break;
+      if (blk + q + NB - 1 < nblk) load(a[(q + NB - 1) % NB], b[(q + NB - 1) % NB], st + (blk + q + NB - 1) * BLK);
+      mma(a[q], b[q]);
+    }
   }
   // D[i = s][j]: lane holds column j = c, rows i = 8 (r / 4) + 4 half + r % 4
 #pragma unroll
@@ -102,24 +107,25 @@ MQ_DEV void dwh_body(Dims d, Lay L, const float* __restrict__ dHYP, const float*
   }
 }
 
-template <int VAR = 0>
+template <int VAR = 0, int NB = 2>
 __global__ __launch_bounds__(256) void dwh_kernel(Dims d, Lay L, const float* __restrict__ dHYP,
                                                   const float* __restrict__ S0, float* __restrict__ slab,
                                                   int64_t len, int nsplit, int tiles_j) {
-  dwh_body<VAR, 8>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, blockIdx.x);
+  dwh_body<VAR, 8, NB>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, blockIdx.x);
 }
 
 // Horizontal fusion: dW_hyper (blocks [0, ndwh)) beside pass 1 of the slab reduction (blocks [ndwh_pad, ..)) in one
 // launch. Neither reads the other's output (pass 1 covers the BPTT's and the mixer's slabs; dW_hyper's own slabs
 // are summed in pass 2, which reads them directly), so the reduction's HBM reads overlap dW_hyper's MFMA chains
 // instead of following them. ndwh_pad is a multiple of 16, so pass 1's block -> XCD mapping is unchanged.
+template <int NB = 2>
 __global__ __launch_bounds__(256) void dwh_red1_kernel(Dims d, Lay L, const float* __restrict__ dHYP,
                                                        const float* __restrict__ S0, float* __restrict__ slab,
                                                        int64_t len, int nsplit, int tiles_j, int ndwh, int ndwh_pad,
                                                        RedPlan pl) {
   const int b = blockIdx.x;
   if (b < ndwh_pad) {
-    if (b < ndwh) dwh_body<0, 8>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, b);
+    if (b < ndwh) dwh_body<0, 8, NB>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, b);
     return;
   }
   red_pass1_body(pl, b - ndwh_pad);

@@ -18,8 +18,10 @@
 // half stage; two staging patterns cover every operand:
 //   KPat: thread -> (row = tid >> 2, k = 4 (tid & 3) + i)   (row-major operand, K contiguous in memory)
 //   MPat: thread -> (row = tid & 63, k = 4 (tid >> 6) + i)  (column operand, rows contiguous in memory)
+//   TPat: thread -> (row = 4 (tid & 15) + i, k = tid >> 4)   (column operand built per K-row, see below)
 // B tiles wider than 64 rows are staged in BN/64 passes of the same pattern.
 #pragma once
+#include <type_traits>
 #include "common.hpp"
 
 namespace mq {
@@ -39,37 +41,70 @@ struct MPat {
 // Row index (within a 32x32 accumulator tile) of register `reg` for `lane` (32x32 f32 MFMA C layout).
 MQ_DEV int acc_row(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 
+// TPat: thread -> (rows 4 (tid & 15) + i, k = tid >> 4)   (transposed: one k, four consecutive rows — an operand
+//   whose natural unit is a K-row of consecutive output columns, e.g. one replay row's agent-input features; a
+//   wave covers 4 K-rows x 64 columns, i.e. four 256-byte row segments per load)
+struct TPat {
+  MQ_DEV static int row(int tid) { return 4 * (tid & 15); }
+  MQ_DEV static int kq(int tid) { return tid >> 4; }
+};
+
 template <class Pat>
 MQ_DEV void stage_store(float* S, const float (&r)[4], int tid, int pass, int half) {
-  *(f32x4*)&S[(64 * pass + Pat::row(tid)) * GLD + GBK * half + Pat::kq(tid)] = f32x4{r[0], r[1], r[2], r[3]};
+  if constexpr (std::is_same<Pat, TPat>::value) {
+    // four b32 stores down a column (rows 4 (tid & 15) + i sit 144 floats = 16 banks apart: 4-way bank conflicts
+    // per store, against one 256-byte global segment per row and wave instead of 64-byte ones)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) S[(64 * pass + TPat::row(tid) + i) * GLD + GBK * half + TPat::kq(tid)] = r[i];
+  } else {
+    *(f32x4*)&S[(64 * pass + Pat::row(tid)) * GLD + GBK * half + Pat::kq(tid)] = f32x4{r[0], r[1], r[2], r[3]};
+  }
 }
 
 #ifdef MQ_GEMM_STAMPS
 __device__ uint64_t* mq_gemm_stamps;   // diagnostic build only (scripts/gemm_micro.hip)
 #endif
 
+// Row passes of a policy's A tile: P::MT when the policy declares it (1 or 2), else 1. With MT = 2 the workgroup
+// owns a 128 x BN tile and each wave a 64 x BN/2 strip (2 x NT accumulators): twice the MFMAs per LDS fragment read
+// and per staged B element, and half the B traffic per row of C.
+template <class P, class = void>
+struct gemm_mt {
+  static constexpr int value = 1;
+};
+template <class P>
+struct gemm_mt<P, std::void_t<decltype(P::MT)>> {
+  static constexpr int value = P::MT;
+};
+
 template <class P>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(const P p) {
-  constexpr int BN = P::BN, NT = BN / 64;
-  __shared__ float As[2][GBM * GLD];
+  constexpr int BN = P::BN, NT = BN / 64, MT = gemm_mt<P>::value, BM = GBM * MT;
+  static_assert(MT == 1 || MT == 2, "MT");
+  __shared__ float As[2][BM * GLD];
   __shared__ float Bs[2][BN * GLD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1, h = lane >> 5;
-  const int m0 = blockIdx.x * GBM, n0 = blockIdx.y * BN, z = blockIdx.z;
-  typename P::Ctx ctx = p.make_ctx(m0, n0, z, tid);
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN, z = blockIdx.z;
+  typename P::Ctx ctx[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) ctx[mt] = p.make_ctx(m0 + GBM * mt, n0, z, tid);
   int kb, ke;
   p.krange(z, kb, ke);
-  f32x16 acc[NT];
+  f32x16 acc[MT][NT];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt)
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[nt][i] = 0.0f;
-  float ra[2][4], rb[2][NT][4], rsum = 0.0f;
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.0f;
+  float ra[2][MT][4], rb[2][NT][4], rsum = 0.0f;
   auto load = [&](int k0) {
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
-      p.load_a(ctx, k0 + GBK * hf, ke, ra[hf]);
 #pragma unroll
-      for (int pp = 0; pp < NT; ++pp) p.load_b(ctx, pp, k0 + GBK * hf, ke, rb[hf][pp]);
+      for (int mt = 0; mt < MT; ++mt) p.load_a(ctx[mt], k0 + GBK * hf, ke, ra[hf][mt]);
+#pragma unroll
+      for (int pp = 0; pp < NT; ++pp) p.load_b(ctx[0], pp, k0 + GBK * hf, ke, rb[hf][pp]);
     }
   };
 #ifdef MQ_GEMM_STAMPS
@@ -83,7 +118,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const P p) {
 #endif
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
-      stage_store<typename P::APat>(As[buf], ra[hf], tid, 0, hf);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) stage_store<typename P::APat>(As[buf], ra[hf][mt], tid, mt, hf);
 #pragma unroll
       for (int pp = 0; pp < NT; ++pp) stage_store<typename P::BPat>(Bs[buf], rb[hf][pp], tid, pp, hf);
     }
@@ -95,25 +131,47 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const P p) {
     ca = __builtin_amdgcn_s_memtime(); cb += ca - cb0;
 #endif
     if (k0 + GSK < ke) load(k0 + GSK);
-    const float* a = As[buf] + (wm * 32 + (lane & 31)) * GLD + 16 * h;
-    f32x4 av[4];
+    if (MT == 1) {
+      const float* a = As[buf] + (wm * 32 + (lane & 31)) * GLD + 16 * h;
+      f32x4 av[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) av[i] = *(const f32x4*)&a[4 * i];
+      for (int i = 0; i < 4; ++i) av[i] = *(const f32x4*)&a[4 * i];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const float* bp = Bs[buf] + (wn * (BN / 2) + nt * 32 + (lane & 31)) * GLD + 16 * h;
-      f32x4 bv[4];
+      for (int nt = 0; nt < NT; ++nt) {
+        const float* bp = Bs[buf] + (wn * (BN / 2) + nt * 32 + (lane & 31)) * GLD + 16 * h;
+        f32x4 bv[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) bv[i] = *(const f32x4*)&bp[4 * i];
+        for (int i = 0; i < 4; ++i) bv[i] = *(const f32x4*)&bp[4 * i];
 #pragma unroll
-      for (int m = 0; m < 16; ++m) acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m >> 2][m & 3], bv[m >> 2][m & 3], acc[nt], 0, 0, 0);
+        for (int m = 0; m < 16; ++m)
+          acc[0][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m >> 2][m & 3], bv[m >> 2][m & 3], acc[0][nt], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const float* bp = Bs[buf] + (wn * (BN / 2) + nt * 32 + (lane & 31)) * GLD + 16 * h;
+        f32x4 bv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bv[i] = *(const f32x4*)&bp[4 * i];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const float* a = As[buf] + (wm * 32 * MT + mt * 32 + (lane & 31)) * GLD + 16 * h;
+          f32x4 av[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) av[i] = *(const f32x4*)&a[4 * i];
+#pragma unroll
+          for (int m = 0; m < 16; ++m)
+            acc[mt][nt] =
+                __builtin_amdgcn_mfma_f32_32x32x2f32(av[m >> 2][m & 3], bv[m >> 2][m & 3], acc[mt][nt], 0, 0, 0);
+        }
+      }
     }
 #ifdef MQ_GEMM_STAMPS
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
     { const uint64_t e = __builtin_amdgcn_s_memtime(); cm += e - ca; }
 #endif
     if (P::kRowSum) {
-      if (blockIdx.y == 0 && tid < GBM) {
+      if (blockIdx.y == 0 && tid < BM) {
         const f32x4* rr = (const f32x4*)&As[buf][tid * GLD];
 #pragma unroll
         for (int i = 0; i < GSK / 4; ++i) rsum += (rr[i][0] + rr[i][1]) + (rr[i][2] + rr[i][3]);
@@ -125,7 +183,10 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const P p) {
   const uint64_t ce0 = __builtin_amdgcn_s_memtime();
 #endif
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) p.epilogue(ctx, acc[nt], m0 + wm * 32, n0 + wn * (BN / 2) + nt * 32, z, lane);
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+      p.epilogue(ctx[mt], acc[mt][nt], m0 + wm * 32 * MT + mt * 32, n0 + wn * (BN / 2) + nt * 32, z, lane);
 #ifdef MQ_GEMM_STAMPS
   if (tid == 0) {
     __builtin_amdgcn_s_waitcnt(0);
@@ -135,13 +196,14 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const P p) {
   }
 #endif
   if (P::kRowSum) {
-    if (blockIdx.y == 0 && tid < GBM) p.rowsum_out(m0 + tid, z, rsum);
+    if (blockIdx.y == 0 && tid < BM) p.rowsum_out(m0 + tid, z, rsum);
   }
 }
 
 template <class P>
 inline hipError_t launch_gemm(const P& p, int M, int N, int Z, hipStream_t s) {
-  dim3 grid((M + GBM - 1) / GBM, (N + P::BN - 1) / P::BN, Z);
+  constexpr int BM = GBM * gemm_mt<P>::value;
+  dim3 grid((M + BM - 1) / BM, (N + P::BN - 1) / P::BN, Z);
   if (grid.x == 0 || grid.y == 0 || grid.z == 0) return hipSuccess;
   hipLaunchKernelGGL(gemm_f32_kernel<P>, grid, dim3(256), 0, s, p);
   return hipGetLastError();

@@ -12,6 +12,7 @@
 // Backward:
 //   Dx1Prob : dP1 = (dGI W_ih) * [X1 > 0]
 //   Dw1Prob : [dW1 | db1] = dP1^T XIN                  split-K over (t, row)
+//   Dw1VProb: the same, xin rebuilt from the replay rows (no XIN copy)
 //   DwhProb : [dW_hyper | db_hyper] = dHYP^T S0        split-K over (t, episode)
 #pragma once
 #include "gemm_f32.hpp"
@@ -28,6 +29,12 @@ MQ_DEV void krange_split(int K, int nsplit, int z, int& kb, int& ke) {
 
 MQ_DEV void ld4(const float* p, float (&r)[4]) {   // 16-B aligned row segment, or zeros
   f32x4 v = p ? *(const f32x4*)p : f32x4{0, 0, 0, 0};
+  r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; r[3] = v[3];
+}
+
+MQ_DEV void ld4u(const float* p, float (&r)[4]) {   // 4-byte aligned row segment: one global_load_dwordx4
+  f32x4 v;
+  __builtin_memcpy(&v, p, sizeof(v));
   r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; r[3] = v[3];
 }
 
@@ -52,6 +59,7 @@ struct Fc1Prob {
   float* X1;   // [2][M][H]
   float* XIN;  // [M][I], written once
   int64_t M;
+  int32_t* rowtab = nullptr;   // [M][4] replay-row table for Dw1VProb (written by the net-0 column block)
   using APat = KPat;
   using BPat = KPat;
   static constexpr bool kRowSum = false;
@@ -74,6 +82,10 @@ struct Fc1Prob {
       c.ag = ag;
       // actions_onehot[t-1] is zero unless slot t-1 was filled (runner contract, synthetic.py)
       if (d.last_action && t > 0 && rp.filled[slot - 1]) c.aprev = (int)rp.actions[(slot - 1) * d.n + ag];
+      if (rowtab && (tid & 3) == 0 && blockIdx.y == 0) {
+        const int64_t off = (slot * d.n + ag) * (int64_t)d.O;
+        *(int4*)(rowtab + 4 * (int64_t)c.m) = int4{(int)(uint32_t)off, (int)(off >> 32), c.aprev, ag};
+      }
     }
     const int nn = KPat::row(tid);   // < H: pass p covers net p's 64 output units
     c.brow[0] = P0 + o_w + (int64_t)nn * d.I;
@@ -83,9 +95,8 @@ struct Fc1Prob {
   MQ_DEV void krange(int, int& kb, int& ke) const { kb = 0; ke = d.I; }
   MQ_DEV void load_a(const Ctx& c, int k0, int ke, float (&r)[4]) const {
     const int k = k0 + KPat::kq(threadIdx.x);
-    if (c.arow && k + 3 < d.O) {   // the common case: four obs features, independent loads
-#pragma unroll
-      for (int i = 0; i < 4; ++i) r[i] = c.arow[k + i];
+    if (c.arow && k + 3 < d.O) {   // the common case: four obs features, one dword-aligned 16-byte load
+      ld4u(c.arow + k, r);
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -178,7 +189,7 @@ struct GiProb {
 
 // Q = Hs W2^T + b2 for both nets (fc2 of rnn_agent.py:35, out of the recurrence).
 struct Fc2Prob {
-  static constexpr int BN = 64;
+  static constexpr int BN = 64;   // MT = 2 measured slower at configs[2] (0.17 -> 0.21 ms, r03)
   const float* Hs;   // [2][M][H]
   const float* P0;
   const float* P1;
@@ -302,7 +313,7 @@ struct HypProb {
 
 // ---------------------------------------------------------------------------------------------- backward
 struct Dx1Prob {
-  static constexpr int BN = 64;
+  static constexpr int BN = 64;   // MT = 2 measured slower in the configs[2] pipeline (0.22 -> 0.31 ms, r03)
   const float* dGI;   // [M][3H]
   const float* Wih;   // online w_ih [3H][H]
   const float* X1o;   // online X1 [M][H]
@@ -377,6 +388,105 @@ struct Dw1Prob {
   }
   MQ_DEV void rowsum_out(int j, int z, float v) const {
     if (j < H) slab[(int64_t)z * (H * I + H) + H * I + j] = v;
+  }
+};
+
+// The same [dW1 | db1] slab with the agent inputs built on the fly from the replay rows (Fc1Prob's gather and
+// one-hot columns) instead of read back from a dense XIN copy: at configs[2] (RT = 625,536, I = 348) that copy is
+// 871 MB written by fc1 and read again here. The B operand is staged per K-row (TPat): thread (k = row tr of the
+// split, four consecutive features f) reads tr's entry of the replay-row table fc1 wrote (16 B: obs row offset,
+// a_{t-1}, agent — 10 MB at configs[2]) and fetches its four inputs with one 16-byte load. Same LDS tile, same k
+// order as Dw1Prob: bitwise the same slab. A/B switch (MQ_DW1_REBUILD=1), not the default: at configs[2] it moves
+// 1.7 GB less per step (fc1 1.18 -> 0.94 ms without the XIN store) but this kernel takes 0.77 ms against
+// Dw1Prob's 0.46 (r03 A/B, profiles/r03_ab_dw1.json): 5.13 vs 5.06 ms a step.
+struct Dw1VProb {
+  static constexpr int BN = 128;
+  Dims d;
+  const float* obs;
+  const int32_t* rowtab;   // [RT][4] from the fc1 pass: obs row offset, a_{t-1}, agent
+  const float* dP1;   // [RT][H]
+  float* slab;        // [nsplit][H*I + H]
+  int64_t K;          // RT
+  int nsplit;
+  using APat = MPat;
+  using BPat = TPat;
+  static constexpr bool kRowSum = true;
+  // The row-table entries of each half stage are fetched one stage ahead (the kernel loads stages in order, each
+  // once; pass 0 of a half stage takes its entry and fetches the next stage's), so the obs load's address never
+  // waits a full memory round trip.
+  struct Ctx {
+    int n0, kb;
+    mutable int4 nxt0, nxt1, cur0, cur1;   // half stage 0 / 1 (named: no dynamically indexed register arrays)
+  };
+  MQ_DEV int4 entry(int m, int ke) const {
+    return m < ke ? *(const int4*)(rowtab + 4 * (int64_t)m) : int4{0, 0, -1, -1};
+  }
+  MQ_DEV Ctx make_ctx(int, int n0, int z, int tid) const {
+    Ctx c;
+    c.n0 = n0;
+    int ke;
+    krange(z, c.kb, ke);
+    c.nxt0 = entry(c.kb + TPat::kq(tid), ke);
+    c.nxt1 = entry(c.kb + GBK + TPat::kq(tid), ke);
+    c.cur0 = c.nxt0;
+    c.cur1 = c.nxt1;
+    return c;
+  }
+  MQ_DEV void krange(int z, int& kb, int& ke) const { krange_split((int)K, nsplit, z, kb, ke); }
+  MQ_DEV void load_a(const Ctx&, int k0, int ke, float (&r)[4]) const {
+    const int j = MPat::row(threadIdx.x), k = k0 + MPat::kq(threadIdx.x);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = (k + i < ke) ? dP1[(int64_t)(k + i) * H + j] : 0.0f;
+  }
+  MQ_DEV void load_b(const Ctx& c, int pass, int k0, int ke, float (&r)[4]) const {
+    const int m = k0 + TPat::kq(threadIdx.x), f0 = c.n0 + 64 * pass + TPat::row(threadIdx.x);
+    const bool h1 = ((k0 - c.kb) & GBK) != 0;   // k0 = kb + GSK * stage + GBK * half
+    if (pass == 0) {
+      if (h1) {
+        c.cur1 = c.nxt1;
+        c.nxt1 = entry(m + GSK, ke);
+      } else {
+        c.cur0 = c.nxt0;
+        c.nxt0 = entry(m + GSK, ke);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = 0.0f;
+    if (m >= ke || f0 >= d.I) return;
+    const int4 e = h1 ? c.cur1 : c.cur0;
+    const float* orow = obs + ((int64_t)(uint32_t)e.x | ((int64_t)e.y << 32));
+    if (f0 + 3 < d.O) {
+      ld4u(orow + f0, r);
+      return;
+    }
+    const int aprev = e.z, ag = e.w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int kk = f0 + i;
+      float v = 0.0f;
+      if (kk < d.O) {
+        v = orow[kk];
+      } else if (kk < d.I) {
+        int f = kk - d.O;
+        if (d.last_action) {
+          if (f < d.A) v = f == aprev ? 1.0f : 0.0f;
+          f -= d.A;
+        }
+        if (f >= 0 && f == ag) v = 1.0f;
+      }
+      r[i] = v;
+    }
+  }
+  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int z, int lane) const {
+    const int f = ncol0 + (lane & 31);
+    if (f >= d.I) return;
+    float* out = slab + (int64_t)z * (H * d.I + H);
+    for_tile(acc, mrow0, ncol0, lane, [&](int j, int ff, float v) {
+      if (j < H) out[(int64_t)j * d.I + ff] = v;
+    });
+  }
+  MQ_DEV void rowsum_out(int j, int z, float v) const {
+    if (j < H) slab[(int64_t)z * (H * d.I + H) + H * d.I + j] = v;
   }
 };
 

@@ -103,6 +103,11 @@ struct mq_handle {
   bool dwh_first = getenv("MQ_DWH_FIRST") && atoi(getenv("MQ_DWH_FIRST")) != 0;
   // A/B switch: dW_hyper as its own launch before the reduction (default: fused with reduction pass 1)
   bool dwh_unfused = getenv("MQ_DWH_UNFUSED") && atoi(getenv("MQ_DWH_UNFUSED")) != 0;
+  // A/B switch: the unfused dW1 rebuilds the agent inputs from the replay rows (Dw1VProb) instead of reading fc1's
+  // dense XIN copy, which fc1 then does not write (learner_gemms.hpp: less traffic, slower at configs[2])
+  bool dw1_xin = !(getenv("MQ_DW1_REBUILD") && atoi(getenv("MQ_DW1_REBUILD")) != 0);
+  // register buffers of dW_hyper's m loop (dwh_kernel.hpp): 4 (default) or 2 (A/B switch MQ_DWH_NB=2)
+  int dwh_nb = getenv("MQ_DWH_NB") && atoi(getenv("MQ_DWH_NB")) == 2 ? 2 : 4;
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
   int slots = 0;
   uint32_t mask = 0;
@@ -284,8 +289,11 @@ hipError_t launch_dwh(mq_handle* h, const Dims& d, const Lay& L, const Work& w, 
   if (side)
     hipLaunchKernelGGL(dwh_side_kernel, dim3(tj * ts * ns), dim3(256), 0, s, d, L, (const float*)w.dHYP,
                        (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj);
+  else if (h->dwh_nb == 2)
+    hipLaunchKernelGGL((dwh_kernel<0, 2>), dim3(tj * ts * ns), dim3(256), 0, s, d, L, (const float*)w.dHYP,
+                       (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj);
   else
-    hipLaunchKernelGGL(dwh_kernel<0>, dim3(tj * ts * ns), dim3(256), 0, s, d, L, (const float*)w.dHYP,
+    hipLaunchKernelGGL((dwh_kernel<0, 4>), dim3(tj * ts * ns), dim3(256), 0, s, d, L, (const float*)w.dHYP,
                        (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj);
   return hipGetLastError();
 }
@@ -333,7 +341,7 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
                           ng(nmix) * (h->E + 1) + ng(nmix) * 8;
   const int64_t norm_parts = (Hd * h->I + Hd + 255) / 256 + (h->len_rnn + 255) / 256 + (h->len_mix + 255) / 256 +
                              (h->E + 1 + 255) / 256 + 1 + 8;
-  int64_t sizes[20] = {
+  int64_t sizes[21] = {
       2 * RT * Hd,                                   // X1
       2 * RT * 3 * Hd,                               // GI
       2 * RT * Hd,                                   // Hs (both nets)
@@ -354,9 +362,10 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
       red_tmp,                                       // two-pass reduction partials
       RT * h->I,                                     // XIN (dense agent inputs)
       Mm * c.state_dim,                              // S0 (gathered state[:, :-1] rows)
+      RT * 4,                                        // rowtab (int32 x 4 per replay row)
   };
-  int64_t total = 0, offs[20];
-  for (int i = 0; i < 20; ++i) { offs[i] = total; total += align_up(std::max<int64_t>(sizes[i], 1)); }
+  int64_t total = 0, offs[21];
+  for (int i = 0; i < 21; ++i) { offs[i] = total; total += align_up(std::max<int64_t>(sizes[i], 1)); }
   hipError_t e = hipMalloc(&h->ws, total * sizeof(float));
   if (e != hipSuccess) {
     delete h;
@@ -374,6 +383,7 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
   w.red_tmp = base + offs[17];
   w.XIN = base + offs[18];
   w.S0 = base + offs[19];
+  w.rowtab = (int32_t*)(base + offs[20]);
   w.curmax = h->curmax_ws;
   *out = h;
   return MQ_OK;
@@ -438,7 +448,9 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
     plan.rw_fwd = rw_fwd;
     pt.begin(PH_FC1);
     {
-      Fc1Prob p{d, rp, h->on, h->tg, h->off[MQ_P_FC1_W], h->off[MQ_P_FC1_B], w.X1, w.XIN, RT};
+      // the dense agent-input copy is written only for a reader: the fused BPTT, or the XIN form of dW1 (A/B)
+      float* xin = fused_bwd || h->dw1_xin ? w.XIN : nullptr;
+      Fc1Prob p{d, rp, h->on, h->tg, h->off[MQ_P_FC1_W], h->off[MQ_P_FC1_B], w.X1, xin, RT, w.rowtab};
       MQ_HIP(launch_gemm(p, (int)RT, 2 * mq::H, 1, s));
     }
     pt.begin(PH_GI);
@@ -551,8 +563,13 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
       int64_t chunk = ((RT + ns - 1) / ns + GBK - 1) / GBK * GBK;
       ns = (int)((RT + chunk - 1) / chunk);
       h->nsplit_fc1 = ns;
-      Dw1Prob p{d.I, w.dP1, w.XIN, w.slab_fc1, RT, ns};
-      MQ_HIP(launch_gemm(p, mq::H, d.I, ns, s));
+      if (h->dw1_xin) {
+        Dw1Prob p{d.I, w.dP1, w.XIN, w.slab_fc1, RT, ns};
+        MQ_HIP(launch_gemm(p, mq::H, d.I, ns, s));
+      } else {   // agent inputs rebuilt from the replay rows (bitwise the XIN form)
+        Dw1VProb p{d, rp.obs, w.rowtab, w.dP1, w.slab_fc1, RT, ns};
+        MQ_HIP(launch_gemm(p, mq::H, d.I, ns, s));
+      }
     }
   }
   // dW_hyper runs fused with pass 1 of the reduction (dwh_red1_kernel) unless an A/B switch placed it elsewhere
@@ -599,8 +616,12 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
     if (dwh_fused) {
       pt.begin(PH_DWH);
       const int ndwh_pad = (ndwh + 15) / 16 * 16;
-      hipLaunchKernelGGL(dwh_red1_kernel, dim3(ndwh_pad + rb.b1), dim3(256), 0, s, d, L, (const float*)w.dHYP,
-                         (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj, ndwh, ndwh_pad, rb.pl);
+      if (h->dwh_nb == 2)
+        hipLaunchKernelGGL(dwh_red1_kernel<2>, dim3(ndwh_pad + rb.b1), dim3(256), 0, s, d, L, (const float*)w.dHYP,
+                           (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj, ndwh, ndwh_pad, rb.pl);
+      else
+        hipLaunchKernelGGL(dwh_red1_kernel<4>, dim3(ndwh_pad + rb.b1), dim3(256), 0, s, d, L, (const float*)w.dHYP,
+                           (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj, ndwh, ndwh_pad, rb.pl);
       MQ_HIP(hipGetLastError());
       pt.begin(PH_RED);
     } else {

@@ -463,6 +463,33 @@ def test_dwh_fused_reduction_bitwise(cases, name, monkeypatch):
     assert outs[0][2] == outs[1][2]
 
 
+@pytest.mark.parametrize("name,unfused", [("wide_qmix", False), ("cfg3_vdn_b128", False), ("tiny_qmix_bare", True),
+                                          ("cfg2_qmix_ragged", True)])
+def test_dw1_rebuilt_inputs_bitwise(cases, name, unfused, monkeypatch):
+    """The unfused dW1 with the agent inputs rebuilt from the replay rows (Dw1VProb, MQ_DW1_REBUILD=1: fc1 writes no
+    dense XIN copy) equals the default dW1 that reads fc1's XIN copy bitwise: last-action / agent-id columns included
+    (tiny_qmix_bare has neither), ragged episodes, device ep-id vectors (wide_qmix) and inline ids."""
+    from tests.gpu_helpers import build, flat_grads, flat_params
+    case = get_case(cases, name)
+    if unfused:
+        for k in UNFUSED_ENV:
+            monkeypatch.setenv(k, "1")
+    outs = []
+    for rebuild in ("0", "1"):
+        monkeypatch.setenv("MQ_DW1_REBUILD", rebuild)
+        args, buf, mac, learner, logger = build(case)
+        np.random.seed(case.sampler_seed)
+        for k in range(2):
+            batch = buf.sample(case.B)
+            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
+        th.cuda.synchronize()
+        outs.append((flat_params(learner), flat_grads(learner), learner.last_stats()))
+        assert learner.last_plan()["fused_bwd"] == 0
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]
+
+
 def test_dwh_split_clamped_when_fused(cases, monkeypatch):
     """MQ_DWH_SPLIT above kRedZ = 16: the fused dW_hyper + reduction-pass-1 launch clamps its m-slices to 16 (its
     slabs must go straight to pass 2, never read by pass-1 blocks of the same grid), so the result is bitwise the
