@@ -18,7 +18,6 @@
 // half stage; two staging patterns cover every operand:
 //   KPat: thread -> (row = tid >> 2, k = 4 (tid & 3) + i)   (row-major operand, K contiguous in memory)
 //   MPat: thread -> (row = tid & 63, k = 4 (tid >> 6) + i)  (column operand, rows contiguous in memory)
-//   TPat: thread -> (row = 4 (tid & 15) + i, k = tid >> 4)   (column operand built per K-row, see below)
 // B tiles wider than 64 rows are staged in BN/64 passes of the same pattern.
 #pragma once
 #include <type_traits>
@@ -41,24 +40,9 @@ struct MPat {
 // Row index (within a 32x32 accumulator tile) of register `reg` for `lane` (32x32 f32 MFMA C layout).
 MQ_DEV int acc_row(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 
-// TPat: thread -> (rows 4 (tid & 15) + i, k = tid >> 4)   (transposed: one k, four consecutive rows — an operand
-//   whose natural unit is a K-row of consecutive output columns, e.g. one replay row's agent-input features; a
-//   wave covers 4 K-rows x 64 columns, i.e. four 256-byte row segments per load)
-struct TPat {
-  MQ_DEV static int row(int tid) { return 4 * (tid & 15); }
-  MQ_DEV static int kq(int tid) { return tid >> 4; }
-};
-
 template <class Pat>
 MQ_DEV void stage_store(float* S, const float (&r)[4], int tid, int pass, int half) {
-  if constexpr (std::is_same<Pat, TPat>::value) {
-    // four b32 stores down a column (rows 4 (tid & 15) + i sit 144 floats = 16 banks apart: 4-way bank conflicts
-    // per store, against one 256-byte global segment per row and wave instead of 64-byte ones)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) S[(64 * pass + TPat::row(tid) + i) * GLD + GBK * half + TPat::kq(tid)] = r[i];
-  } else {
-    *(f32x4*)&S[(64 * pass + Pat::row(tid)) * GLD + GBK * half + Pat::kq(tid)] = f32x4{r[0], r[1], r[2], r[3]};
-  }
+  *(f32x4*)&S[(64 * pass + Pat::row(tid)) * GLD + GBK * half + Pat::kq(tid)] = f32x4{r[0], r[1], r[2], r[3]};
 }
 
 #ifdef MQ_GEMM_STAMPS

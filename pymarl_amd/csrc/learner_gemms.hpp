@@ -59,7 +59,7 @@ struct Fc1Prob {
   float* X1;   // [2][M][H]
   float* XIN;  // [M][I], written once
   int64_t M;
-  int32_t* rowtab = nullptr;   // [M][4] replay-row table for Dw1VProb (written by the net-0 column block)
+  int32_t* rowtab = nullptr;   // [M][2] replay-row table for Dw1VProb (written by the net-0 column block)
   using APat = KPat;
   using BPat = KPat;
   static constexpr bool kRowSum = false;
@@ -82,10 +82,8 @@ struct Fc1Prob {
       c.ag = ag;
       // actions_onehot[t-1] is zero unless slot t-1 was filled (runner contract, synthetic.py)
       if (d.last_action && t > 0 && rp.filled[slot - 1]) c.aprev = (int)rp.actions[(slot - 1) * d.n + ag];
-      if (rowtab && (tid & 3) == 0 && blockIdx.y == 0) {
-        const int64_t off = (slot * d.n + ag) * (int64_t)d.O;
-        *(int4*)(rowtab + 4 * (int64_t)c.m) = int4{(int)(uint32_t)off, (int)(off >> 32), c.aprev, ag};
-      }
+      if (rowtab && (tid & 3) == 0 && blockIdx.y == 0)
+        *(int2*)(rowtab + 2 * (int64_t)c.m) = int2{(int)(slot * d.n + ag), (c.aprev + 1) | (ag << 16)};
     }
     const int nn = KPat::row(tid);   // < H: pass p covers net p's 64 output units
     c.brow[0] = P0 + o_w + (int64_t)nn * d.I;
@@ -393,43 +391,46 @@ struct Dw1Prob {
 
 // The same [dW1 | db1] slab with the agent inputs built on the fly from the replay rows (Fc1Prob's gather and
 // one-hot columns) instead of read back from a dense XIN copy: at configs[2] (RT = 625,536, I = 348) that copy is
-// 871 MB written by fc1 and read again here. The B operand is staged per K-row (TPat): thread (k = row tr of the
-// split, four consecutive features f) reads tr's entry of the replay-row table fc1 wrote (16 B: obs row offset,
-// a_{t-1}, agent — 10 MB at configs[2]) and fetches its four inputs with one 16-byte load. Same LDS tile, same k
-// order as Dw1Prob: bitwise the same slab. A/B switch (MQ_DW1_REBUILD=1), not the default: at configs[2] it moves
-// 1.7 GB less per step (fc1 1.18 -> 0.94 ms without the XIN store) but this kernel takes 0.77 ms against
-// Dw1Prob's 0.46 (r03 A/B, profiles/r03_ab_dw1.json): 5.13 vs 5.06 ms a step.
+// 871 MB written by fc1 and read again here. The B operand is staged like Dw1Prob's (MPat); each K-row (row tr of the
+// split) reads tr's entry of the replay-row table fc1 wrote (8 B: obs row, a_{t-1}, agent — 5 MB at configs[2]).
+// Same LDS tile, same k order as Dw1Prob: bitwise the same slab. A/B switch (MQ_DW1_REBUILD=1), not the default:
+// at configs[2] it moves
+// 1.7 GB less per step (fc1 1.17 -> 0.93 ms without the XIN store) but this kernel takes 0.74 ms against
+// Dw1Prob's 0.46 (r03 A/B, profiles/r03_ab_dw1.json): 5.08 vs 5.04 ms a step. Its loads are instruction for
+// instruction Dw1Prob's (same staging, SGPR row bases); what differs is the memory side: XIN is one dense 871 MB
+// stream, the obs rows are 31 KB runs (27 agents x 285 floats of one episode) scattered over the 28 GB replay.
 struct Dw1VProb {
   static constexpr int BN = 128;
   Dims d;
   const float* obs;
-  const int32_t* rowtab;   // [RT][4] from the fc1 pass: obs row offset, a_{t-1}, agent
+  const int32_t* rowtab;   // [RT][2] from the fc1 pass: obs row index, (a_{t-1} + 1) | agent << 16
   const float* dP1;   // [RT][H]
   float* slab;        // [nsplit][H*I + H]
   int64_t K;          // RT
   int nsplit;
   using APat = MPat;
-  using BPat = TPat;
+  using BPat = MPat;
   static constexpr bool kRowSum = true;
-  // The row-table entries of each half stage are fetched one stage ahead (the kernel loads stages in order, each
-  // once; pass 0 of a half stage takes its entry and fetches the next stage's), so the obs load's address never
-  // waits a full memory round trip.
+  // Wave w stages K-rows 4w .. 4w + 3 of each half stage, so the four replay rows it needs are wave-uniform: their
+  // table entries are fetched one stage ahead into VGPRs (nxt*), moved to SGPRs (readfirstlane) when the stage is
+  // staged, and each obs element is then a load from an SGPR row base at the lane's feature offset: the same
+  // 256-byte segments per row as Dw1Prob reads from XIN, with no per-lane address arithmetic.
   struct Ctx {
     int n0, kb;
-    mutable int4 nxt0, nxt1, cur0, cur1;   // half stage 0 / 1 (named: no dynamically indexed register arrays)
+    mutable int2 nxt0[4], nxt1[4];   // half stage 0 / 1, K-rows 4w + i (static indices only)
   };
-  MQ_DEV int4 entry(int m, int ke) const {
-    return m < ke ? *(const int4*)(rowtab + 4 * (int64_t)m) : int4{0, 0, -1, -1};
-  }
+  MQ_DEV int2 entry(int m, int ke) const { return m < ke ? *(const int2*)(rowtab + 2 * (int64_t)m) : int2{0, 0}; }
   MQ_DEV Ctx make_ctx(int, int n0, int z, int tid) const {
     Ctx c;
     c.n0 = n0;
     int ke;
     krange(z, c.kb, ke);
-    c.nxt0 = entry(c.kb + TPat::kq(tid), ke);
-    c.nxt1 = entry(c.kb + GBK + TPat::kq(tid), ke);
-    c.cur0 = c.nxt0;
-    c.cur1 = c.nxt1;
+    const int mb = c.kb + 4 * (tid >> 6);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      c.nxt0[i] = entry(mb + i, ke);
+      c.nxt1[i] = entry(mb + GBK + i, ke);
+    }
     return c;
   }
   MQ_DEV void krange(int z, int& kb, int& ke) const { krange_split((int)K, nsplit, z, kb, ke); }
@@ -439,44 +440,50 @@ struct Dw1VProb {
     for (int i = 0; i < 4; ++i) r[i] = (k + i < ke) ? dP1[(int64_t)(k + i) * H + j] : 0.0f;
   }
   MQ_DEV void load_b(const Ctx& c, int pass, int k0, int ke, float (&r)[4]) const {
-    const int m = k0 + TPat::kq(threadIdx.x), f0 = c.n0 + 64 * pass + TPat::row(threadIdx.x);
-    const bool h1 = ((k0 - c.kb) & GBK) != 0;   // k0 = kb + GSK * stage + GBK * half
-    if (pass == 0) {
-      if (h1) {
-        c.cur1 = c.nxt1;
-        c.nxt1 = entry(m + GSK, ke);
-      } else {
-        c.cur0 = c.nxt0;
-        c.nxt0 = entry(m + GSK, ke);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int mb = k0 + 4 * wv;                                  // wave-uniform first K-row
+    const int f = c.n0 + 64 * pass + (threadIdx.x & 63);
+    const bool h1 = ((k0 - c.kb) & GBK) != 0;                    // k0 = kb + GSK * stage + GBK * half
+    int row[4], aux[4];
+    if (h1) {   // uniform branch: the arrays are only ever indexed with constants
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        row[i] = __builtin_amdgcn_readfirstlane(c.nxt1[i].x);
+        aux[i] = __builtin_amdgcn_readfirstlane(c.nxt1[i].y);
+        if (pass == NT_LAST) c.nxt1[i] = entry(mb + GSK + i, ke);   // last pass: fetch the next stage's entries
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        row[i] = __builtin_amdgcn_readfirstlane(c.nxt0[i].x);
+        aux[i] = __builtin_amdgcn_readfirstlane(c.nxt0[i].y);
+        if (pass == NT_LAST) c.nxt0[i] = entry(mb + GSK + i, ke);
       }
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = 0.0f;
-    if (m >= ke || f0 >= d.I) return;
-    const int4 e = h1 ? c.cur1 : c.cur0;
-    const float* orow = obs + ((int64_t)(uint32_t)e.x | ((int64_t)e.y << 32));
-    if (f0 + 3 < d.O) {
-      ld4u(orow + f0, r);
-      return;
-    }
-    const int aprev = e.z, ag = e.w;
+    const bool plain = c.n0 + 64 * pass + 63 < d.O;             // uniform: every lane's feature is an obs column
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int kk = f0 + i;
       float v = 0.0f;
-      if (kk < d.O) {
-        v = orow[kk];
-      } else if (kk < d.I) {
-        int f = kk - d.O;
-        if (d.last_action) {
-          if (f < d.A) v = f == aprev ? 1.0f : 0.0f;
-          f -= d.A;
+      if (mb + i < ke) {
+        const float* orow = obs + (int64_t)row[i] * d.O;
+        if (plain) {
+          v = orow[f];
+        } else if (f < d.O) {
+          v = orow[f];
+        } else if (f < d.I) {
+          int fo = f - d.O;
+          const int aprev = (aux[i] & 0xffff) - 1, ag = aux[i] >> 16;
+          if (d.last_action) {
+            if (fo < d.A) v = fo == aprev ? 1.0f : 0.0f;
+            fo -= d.A;
+          }
+          if (fo >= 0 && fo == ag) v = 1.0f;
         }
-        if (f >= 0 && f == ag) v = 1.0f;
       }
       r[i] = v;
     }
   }
+  static constexpr int NT_LAST = BN / 64 - 1;
   MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int z, int lane) const {
     const int f = ncol0 + (lane & 31);
     if (f >= d.I) return;
