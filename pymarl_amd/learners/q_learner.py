@@ -181,13 +181,14 @@ class QLearner:
         if self.mixer is not None and hasattr(self.mixer, "_flat"):
             self.mixer._flat = self._online[Pa:self.n_params]
             self.target_mixer._flat = self._target[Pa:self.n_params]
+        self._step_t = th.tensor(float(getattr(self, "_opt_steps", 0)))
         o = 0
         for p in self.params:
             n = p.numel()
             p.grad = self._grad[o:o + n].view_as(p)
             st = self.optimiser.state[p]
             st["square_avg"] = self._sq[o:o + n].view_as(p)
-            st["step"] = th.tensor(float(self._opt_steps if hasattr(self, "_opt_steps") else 0))
+            st["step"] = self._step_t   # one shared counter: train() increments it once, not once per parameter
             o += n
         self._handle = None
 
@@ -239,8 +240,7 @@ class QLearner:
             allreduce_grad_buffer(self._grad)
         _lib.check(lib.mq_apply(h.h, s))
         self._opt_steps += 1
-        for p in self.params:
-            self.optimiser.state[p]["step"] += 1
+        self._step_t += 1   # every parameter's optimiser state holds this tensor (see save_models)
         self._last_batch = (batch.batch_size, rep.t_len)
         del keep
 
@@ -278,7 +278,11 @@ class QLearner:
         self.mac.save_models(path)
         if self.mixer is not None:
             th.save(self.mixer.state_dict(), "{}/mixer.th".format(path))
-        th.save(self.optimiser.state_dict(), "{}/opt.th".format(path))
+        # per-parameter step tensors in the file, as torch's RMSprop writes them: the live state shares one counter,
+        # and a loader that kept it shared would count every parameter's update into it
+        sd = self.optimiser.state_dict()
+        sd["state"] = {i: dict(v, step=v["step"].clone()) if "step" in v else v for i, v in sd["state"].items()}
+        th.save(sd, "{}/opt.th".format(path))
 
     def load_models(self, path):
         self.mac.load_models(path)
