@@ -575,3 +575,12 @@ def main():
 
 if __name__ == "__main__":
     main()
+    # release the learners' library handles (cycles included) while the HIP runtime — and a profiler's interception
+    # layer, when one is loaded — is still up, not from interpreter-exit finalisers (a cfg5 run under rocprofv3
+    # crashed in exit-time teardown after writing its results)
+    import gc
+    gc.collect()
+    if "torch" in sys.modules:
+        import torch as _th
+        if _th.cuda.is_initialized():
+            _th.cuda.synchronize()
