@@ -87,6 +87,10 @@ struct mq_handle {
   int nsplit_fc1 = 1, nsplit_mix = 1, nblk_bwd = 1, nblk_mix = 1, n_norm_part = 0;
   bool force_unfused = getenv("MQ_UNFUSED_FWD") != nullptr;       // A/B switch for the fused agent forward
   bool force_unfused_bwd = getenv("MQ_UNFUSED_BWD") != nullptr;   // A/B switch for the fused BPTT
+  // rows up to which the fused BPTT (one row per workgroup, one workgroup per CU) is used: past the CU count the
+  // rows run as a second wave of workgroups, which still beats gru_bwd<2> + dX1 + dW1 at configs[3]'s shard
+  // (R = 320); MQ_FUSED_BWD_RMAX=256 restores the round-2 cut-over for A/B runs
+  int fused_bwd_rmax = getenv("MQ_FUSED_BWD_RMAX") ? atoi(getenv("MQ_FUSED_BWD_RMAX")) : 512;
   bool force_unfused_mix = getenv("MQ_GEMM_HYPER") != nullptr;   // A/B switch: hypernet through gemm_f32
   int dwh_split = getenv("MQ_DWH_SPLIT") ? atoi(getenv("MQ_DWH_SPLIT")) : 8;   // m-slices of the dW_hyper pass
   bool generic_mix = getenv("MQ_GENERIC_MIX") != nullptr;   // A/B switch: mix_kernel instead of mix_fast_kernel
@@ -436,7 +440,7 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
   plan.rows = d.R;
   plan.inline_ids = rp.nids > 0 ? 1 : 0;
   const int rw_bwd = std::min(2, pick_rw(d.R, 256));
-  const bool fused_bwd = rw_bwd == 1 && fused_bwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused_bwd;
+  const bool fused_bwd = d.R <= h->fused_bwd_rmax && fused_bwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused_bwd;
   const int rw_fwd = pick_rw(d.R, 512);
   if (rw_fwd == 1 && fused_fwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused) {
     plan.fused_fwd = 1;

@@ -215,7 +215,7 @@ def test_cfg2_trajectory(cases, name):
 
 # Kernel variants past the fused kernels' limits, each pinned to a reference golden run (tests/golden/make_golden.py)
 # and to the oracle teacher-forced: R = B * n rows selects gru_fwd_kernel<RW> (RW = 2 / 4 / 8 rows per workgroup)
-# and gru_bwd_kernel<2>; B > 256 sends the episode ids through the device vector; cfg3_vdn_b128 is BASELINE
+# and gru_bwd_kernel<2> (R > 512); B > 256 sends the episode ids through the device vector; cfg3_vdn_b128 is BASELINE
 # configs[2] itself (the bench's cfg3 path).
 WIDE_PLANS = {
     "rw2_qmix": dict(rows=576, fused_fwd=0, rw_fwd=2, fused_bwd=0, rw_bwd=2, inline_ids=1, hyper="ws"),
@@ -223,6 +223,8 @@ WIDE_PLANS = {
     "wide_qmix": dict(rows=2400, fused_fwd=0, rw_fwd=8, fused_bwd=0, rw_bwd=2, inline_ids=0),
     "cfg3_vdn_b128": dict(rows=3456, fused_fwd=0, rw_fwd=8, fused_bwd=0, rw_bwd=2, inline_ids=1, mix="generic"),
     "cfg2_iql": dict(rows=256, fused_fwd=1, fused_bwd=1, hyper="none"),
+    # configs[3]'s per-GPU shard: R = 320 rows, past the CU count, still on the fused BPTT (a second wave of rows)
+    "cfg4_qmix": dict(rows=320, fused_fwd=1, fused_bwd=1, hyper="ws"),
 }
 
 
