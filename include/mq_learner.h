@@ -92,6 +92,8 @@ int mq_bind(mq_handle* h, float* online, float* target, float* grad, float* sq_a
 int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream);
 /* Normalise by sum(m), clip_grad_norm_(grad_norm_clip), RMSprop(lr, alpha, eps) step, write stats. */
 int mq_apply(mq_handle* h, void* stream);
+/* mq_forward_backward + mq_apply in one call. With MQ_FUSED_APPLY=1 in the environment at mq_create and no data
+ * parallelism, the reduction's last pass and the optimiser step run as one launch (bitwise the two calls'). */
 int mq_train_step(mq_handle* h, const mq_replay* batch, void* stream);
 /* Declare that the caller sums the gradient buffer across ranks between mq_forward_backward and mq_apply
  * (mq_apply then recomputes the global gradient norm from the reduced buffer). */

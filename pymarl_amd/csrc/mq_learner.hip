@@ -103,6 +103,13 @@ struct mq_handle {
   bool dwh_overlap = getenv("MQ_DWH_OVERLAP") && atoi(getenv("MQ_DWH_OVERLAP")) != 0;
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // A/B switch, off by default: mq_train_step runs reduction pass 2 and the optimiser step as one launch
+  // (red_pass2_apply_kernel) unless data parallel. Measured at cfg2 (profiles/r03d_ab_fused_apply): bitwise equal,
+  // 13.2-13.5 us against 12.9-13.1 us for the two launches: the ticket hand-off costs what the launch it removes did
+  bool fuse_apply = getenv("MQ_FUSED_APPLY") && atoi(getenv("MQ_FUSED_APPLY")) == 1;
+  unsigned* ticket = nullptr;   // the fused launch's arrival counter (never reset: tickets continue from ticket_base)
+  unsigned ticket_base = 0;
+  int apply_cap = -1;           // co-resident blocks of red_pass2_apply_kernel (-1: not queried yet)
   // A/B switch: dW_hyper launched between the mixer and the BPTT instead of after the BPTT (same stream)
   bool dwh_first = getenv("MQ_DWH_FIRST") && atoi(getenv("MQ_DWH_FIRST")) != 0;
   // A/B switch: dW_hyper as its own launch before the reduction (default: fused with reduction pass 1)
@@ -399,6 +406,7 @@ int mq_destroy(mq_handle* h) {
   for (auto e : h->ev1) (void)hipEventDestroy(e);
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  if (h->ticket) (void)hipFree(h->ticket);
   if (h->side) (void)hipStreamDestroy(h->side);
   if (h->ws) (void)hipFree(h->ws);
   if (h->comm && h->comm_owned) (void)ncclCommDestroy(h->comm);
@@ -420,13 +428,52 @@ int mq_bind(mq_handle* h, float* online, float* target, float* grad, float* sq_a
   return MQ_OK;
 }
 
+namespace {
+
+// Whether red_pass2_apply_kernel's grid of nb blocks is co-resident (its tail blocks wait for the others): the
+// occupancy query less one block per CU (the query can run one high, MI355X_MICROARCH.md hazards), times the CUs.
+bool pass2_apply_resident(mq_handle* h, int nb) {
+  if (h->apply_cap < 0) {
+    int dev = 0, ncu = 0, per = 0;
+    h->apply_cap = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, red_pass2_apply_kernel, 256, 0) == hipSuccess)
+      h->apply_cap = std::max(per - 1, 0) * ncu;
+  }
+  return nb >= 1 && nb <= h->apply_cap;
+}
+
+}  // namespace
+
+static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fuse_req, bool* fused_apply);
+
 int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
+  bool fused = false;
+  return fb_impl(h, batch, (hipStream_t)stream, false, &fused);
+}
+
+int mq_train_step(mq_handle* h, const mq_replay* batch, void* stream) {
+  if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
+  // the optimiser step needs the whole (all-reduced) gradient: with data parallelism it stays a separate pass
+  const bool fuse = !h->dp && !h->comm && h->fuse_apply;
+  bool fused = false;
+  int rc = fb_impl(h, batch, (hipStream_t)stream, fuse, &fused);
+  if (rc) return rc;
+  if (fused) {
+    ++h->tstep;
+    return MQ_OK;
+  }
+  return mq_apply(h, stream);
+}
+
+static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fuse_req, bool* fused_apply) {
+  *fused_apply = false;
   if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
   if (!h->on || !h->tg || !h->grad || !h->sq || !h->stats)
     return set_err(MQ_ERR_STATE, "training needs online, target, grad, sq_avg and stats bound (mq_bind)");
   int rc = check_batch(h, batch);
   if (rc) return rc;
-  hipStream_t s = (hipStream_t)stream;
   const Dims d = make_dims(h, batch);
   const Rep rp = make_rep(batch);
   const Lay L = make_lay(h);
@@ -635,12 +682,29 @@ int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
         MQ_HIP(hipGetLastError());
       }
     }
-    hipLaunchKernelGGL(red_pass2_kernel, dim3(rb.b2), dim3(256), 0, s, rb.pl, w.norm_part);
-    MQ_HIP(hipGetLastError());
+    // applying blocks: kApplyTail, or enough that kApplyMaxE elements per thread cover the parameters
+    const int tail = (int)std::max<int64_t>(std::min(kApplyTail, rb.b2), (h->P + 256 * kApplyMaxE - 1) / (256 * kApplyMaxE));
+    if (fuse_req && tail <= rb.b2 && pass2_apply_resident(h, rb.b2)) {
+      if (!h->ticket) {
+        MQ_HIP(hipMalloc(&h->ticket, 256));
+        MQ_HIP(hipMemset(h->ticket, 0, 256));
+        h->ticket_base = 0;
+      }
+      // pass 2 and the optimiser step in one launch (optim_kernels.hpp)
+      const OptHP hp{h->cfg.lr, h->cfg.optim_alpha, h->cfg.optim_eps, h->cfg.grad_norm_clip, h->cfg.n_agents};
+      hipLaunchKernelGGL(red_pass2_apply_kernel, dim3(rb.b2), dim3(256), 0, s, rb.pl, w.norm_part, h->ticket,
+                         h->ticket_base, tail, h->on, h->grad, h->sq, h->P, hp, h->stats);
+      MQ_HIP(hipGetLastError());
+      h->ticket_base += (unsigned)rb.b2;
+      *fused_apply = true;
+    } else {
+      hipLaunchKernelGGL(red_pass2_kernel, dim3(rb.b2), dim3(256), 0, s, rb.pl, w.norm_part);
+      MQ_HIP(hipGetLastError());
+    }
     h->n_norm_part = rb.b2;
   }
   pt.end();
-  if (h->comm) {   // native data parallelism: the whole [grads | sums] buffer, summed over the ranks in stream order
+  if (h->comm && !*fused_apply) {   // native data parallelism: the whole [grads | sums] buffer, summed over the ranks in stream order
     const ncclResult_t r = ncclAllReduce(h->grad, h->grad, (size_t)(h->P + MQ_NSUMS), ncclFloat, ncclSum, h->comm, s);
     if (r != ncclSuccess) return set_err(MQ_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
   }
@@ -750,12 +814,6 @@ int mq_comm_detach(mq_handle* h) {
   h->comm_world = 0;
   h->comm_owned = false;
   return MQ_OK;
-}
-
-int mq_train_step(mq_handle* h, const mq_replay* batch, void* stream) {
-  int rc = mq_forward_backward(h, batch, stream);
-  if (rc) return rc;
-  return mq_apply(h, stream);
 }
 
 int mq_update_targets(mq_handle* h, void* stream) {

@@ -235,10 +235,13 @@ class QLearner:
             h.dp_on = want
         rep, keep = replay_view(batch)
         lib, s = h.lib, _lib.stream_ptr()
-        _lib.check(lib.mq_forward_backward(h.h, ctypes.byref(rep), s))   # + the native all-reduce when attached
         if dp and not h.native:
+            _lib.check(lib.mq_forward_backward(h.h, ctypes.byref(rep), s))
             allreduce_grad_buffer(self._grad)
-        _lib.check(lib.mq_apply(h.h, s))
+            _lib.check(lib.mq_apply(h.h, s))
+        else:
+            # one call: mq_forward_backward (+ the native all-reduce when attached) and mq_apply
+            _lib.check(lib.mq_train_step(h.h, ctypes.byref(rep), s))
         self._opt_steps += 1
         self._step_t += 1   # every parameter's optimiser state holds this tensor (see save_models)
         self._last_batch = (batch.batch_size, rep.t_len)

@@ -80,6 +80,7 @@ def test_train_without_handle_bound_reports_state_error():
     lib = _lib.load()
     assert lib.mq_apply(None, None) != 0
     assert lib.mq_forward_backward(None, None, None) != 0
+    assert lib.mq_train_step(None, None, None) != 0
     assert lib.mq_last_plan(None, ctypes.byref(_lib.MQPlan())) != 0
 
 

@@ -492,6 +492,30 @@ def test_dw1_rebuilt_inputs_bitwise(cases, name, unfused, monkeypatch):
     assert outs[0][2] == outs[1][2]
 
 
+@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_vdn", "tiny_qmix_full", "cfg4_qmix"])
+def test_fused_pass2_apply_bitwise(cases, name, monkeypatch):
+    """mq_train_step without data parallelism runs reduction pass 2 and the RMSprop step as one launch
+    (red_pass2_apply_kernel: ticket counter, the last blocks to arrive apply); parameters, clipped gradients,
+    square_avg and the five stats equal the two-launch path (MQ_FUSED_APPLY=0) bitwise over up to three steps."""
+    from tests.gpu_helpers import build, flat_grads, flat_params
+    case = get_case(cases, name)
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("MQ_FUSED_APPLY", fused)
+        args, buf, mac, learner, logger = build(case)
+        np.random.seed(case.sampler_seed)
+        for k in range(min(3, len(case.episodes))):
+            batch = buf.sample(case.B)
+            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
+        th.cuda.synchronize()
+        outs.append((flat_params(learner), flat_grads(learner), learner._sq.cpu().numpy(), learner.last_stats()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert np.array_equal(outs[0][2], outs[1][2])
+    assert outs[0][3] == outs[1][3]
+    assert all(np.isfinite(v) for v in outs[0][3].values() if isinstance(v, float))
+
+
 def test_dwh_split_clamped_when_fused(cases, monkeypatch):
     """MQ_DWH_SPLIT above kRedZ = 16: the fused dW_hyper + reduction-pass-1 launch clamps its m-slices to 16 (its
     slabs must go straight to pass 2, never read by pass-1 blocks of the same grid), so the result is bitwise the
