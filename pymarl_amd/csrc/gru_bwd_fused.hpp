@@ -66,7 +66,8 @@ inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_
 // accumulator pairs in the W_hh^T mat-vec, 8192 per-phase cycle budget of the chain step (s_memtime stamps of chain
 // wave 0: inputs + gate math + LDS stores | barrier | LDS reads of dgh | W_hh^T FMAs | DPP quad reduction + W2
 // lookup), summed over the steps into w.slab_mix[32 * block + 17 ..] (diagnostic, scripts/chain_micro.hip), 16384
-// the K12 mat-vec layout (below), 32768 decoupled roles (below), 65536 the linearised step (below).
+// the K12 mat-vec layout (below), 32768 decoupled roles (below), 65536 the linearised step (below), 262144 the K12
+// W_hh^T prologue as one dword load per weight (A/B; default: one 16-byte load per row).
 //
 // Linearised step (VAR 65536). Every gate derivative of a step is dh times a coefficient of that step's inputs:
 // dn = dh (1 - z), dz = dh (h_{t-1} - n), d(a_n) = dh (1 - z)(1 - n^2), d(a_r) = d(a_n) ghn r (1 - r),
@@ -160,11 +161,26 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
         const int b3 = (c16 >> 3) & 1, b2 = (c16 >> 2) & 1, u0 = 4 * (lt >> 4);
         const int a0 = u0 + 2 * b3 + b2, a1 = u0 + 2 * b3 + 1 - b2;               // pair A: the units kept
         const int v0 = u0 + 2 * (1 - b3) + b2, v1 = u0 + 2 * (1 - b3) + 1 - b2;   // pair B: the partner's
+        if (VAR & 262144) {   // A/B: the round-3 prologue, one dword load per weight
 #pragma unroll
-        for (int kk = 0; kk < 12; ++kk) {
-          const float* wr = Whh + (12 * c16 + kk) * H;
-          wT[2 * kk] = f32x2{wr[a0], wr[a1]};
-          wT[2 * kk + 1] = f32x2{wr[v0], wr[v1]};
+          for (int kk = 0; kk < 12; ++kk) {
+            const float* wr = Whh + (12 * c16 + kk) * H;
+            wT[2 * kk] = f32x2{wr[a0], wr[a1]};
+            wT[2 * kk + 1] = f32x2{wr[v0], wr[v1]};
+          }
+        } else {
+          // units a0, a1, v0, v1 are u0 .. u0 + 3 in a lane-dependent order: one 16-byte load per row (the
+          // compiler cannot merge the four lane-permuted dword loads itself), then selects
+          auto pick = [](const f32x4& x, int i) { return i == 0 ? x[0] : i == 1 ? x[1] : i == 2 ? x[2] : x[3]; };
+          const int i0 = a0 - u0, i1 = a1 - u0, i2 = v0 - u0, i3 = v1 - u0;
+          f32x4 xr[12];
+#pragma unroll
+          for (int kk = 0; kk < 12; ++kk) xr[kk] = *(const f32x4*)(Whh + (12 * c16 + kk) * H + u0);
+#pragma unroll
+          for (int kk = 0; kk < 12; ++kk) {
+            wT[2 * kk] = f32x2{pick(xr[kk], i0), pick(xr[kk], i1)};
+            wT[2 * kk + 1] = f32x2{pick(xr[kk], i2), pick(xr[kk], i3)};
+          }
         }
       } else {
 #pragma unroll
@@ -718,6 +734,9 @@ inline void launch_bwd_fused(dim3 grid, size_t dyn, hipStream_t s, const Dims& d
                        slab1_len);
   else if (var == 768 + 65536)   // linearised step
     hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 65536>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else if (var == 768 + 65536 + 16384 + 262144)   // production with dword W_hh^T prologue loads (A/B)
+    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 65536 + 16384 + 262144>, grid, dim3(512), dyn, s, d, rp, P, L, w,
+                       slab_len, slab1_len);
   else if (var == 768 + 65536 + 16384)   // linearised step + K12
     hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 65536 + 16384>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len,
                        slab1_len);
