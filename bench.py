@@ -355,6 +355,21 @@ def dist_info(world, learner=None, what="all_reduce(sum) of the fused [grads | s
     return {"world_size": 1, "backend": None, "collective": None}
 
 
+def release_handles(*objs):
+    """Destroy the library handles these objects own (mc_destroy / mq_destroy: side streams, events, communicators)
+    now, with the HIP runtime and any profiler's interception layer still up, instead of in interpreter-exit
+    teardown (a cfg5 run under rocprofv3 crashed there after writing its results)."""
+    import gc
+    import torch as th
+    th.cuda.synchronize()
+    for o in objs:
+        for attr in ("_handle", "_mac_handle", "_policy_handle"):
+            if getattr(o, attr, None) is not None:
+                setattr(o, attr, None)
+    gc.collect()
+    th.cuda.synchronize()
+
+
 def coma_bench(a):
     """cfg5: COMALearner.train on coma_smac's batch of B = 8 episodes (MMM2 shape: 80 critic rows). N > 1 is strong
     scaling of that batch: every rank passes the same global sample, runs the critic's T dependent optimiser steps
@@ -406,6 +421,7 @@ def coma_bench(a):
     achieved = step_flops / (chain_ms * 1e-3 / T) / 1e12
     value = B * T * n * a.steps / dt
     if rank != 0:
+        release_handles(learner, mac)
         dist.destroy_process_group()
         return
     cpu = None if (a.no_cpu_baseline or world > 1) else coma_cpu_baseline(a.config, data)
@@ -429,7 +445,8 @@ def coma_bench(a):
                      "phases_ms": {k: float(np.mean([c[k] for c in chains])) for k in chains[0]}},
         "cpu_baseline": cpu,
     }
-    print(json.dumps(line))
+    print(json.dumps(line), flush=True)
+    release_handles(learner, mac)
     if world > 1:
         dist.destroy_process_group()
 
