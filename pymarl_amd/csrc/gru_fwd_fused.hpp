@@ -23,6 +23,7 @@
 #pragma once
 #include <cstdlib>
 #include "gru_kernels.hpp"
+#include "learner_gemms.hpp"
 
 namespace mq {
 
@@ -56,6 +57,126 @@ struct FusedLds {
   int aprev[FCH];
 };
 
+// ---- QMIX hypernet workgroups appended to the fused forward's grid (HYP = 1): hyper_ws_kernel's GEMM (same
+// operand maps, K order and outputs: bitwise its HYP and S0) in a forward workgroup's shape — 512 threads, the
+// forward's 128-VGPR budget, its static LDS (one weight-chunk buffer instead of two). Dispatched after every
+// row-net of the forward, these workgroups take CU slots as row-nets finish: beside the second row-net of a CU at
+// cfg2 (forward + hypernet LDS fit one CU), on the CUs a second wave of row-nets leaves idle at configs[3]'s shard;
+// and the hypernet launch is gone. 4 loader waves stream 64-row chunks (the fetch of chunk c + 1 overlaps chunk c's
+// MFMAs; staging waits for them), 4 MFMA waves own one N-tile of a chunk for both 16-row M-tiles.
+constexpr int HYF_SP = 4 * 48 + 4;   // state-row pitch (hyper_kernel.hpp HYWS_SP)
+constexpr int HYF_GS = 48 * 64;      // one 16-row weight group (HYWS_GS)
+__host__ __device__ constexpr int hyf_floats() { return 32 * HYF_SP + 4 * HYF_GS + 1024; }
+inline bool hyf_ok(int S, int E, int NH, int64_t M) {
+  return S <= 192 && S % 4 == 0 && E % 16 == 0 && NH <= 1024 && M * NH * 4 < (1LL << 31);
+}
+
+MQ_DEV void hyper_fwd_body(const Dims& d, const Rep& rp, const float* __restrict__ P0, const float* __restrict__ P1,
+                           const Lay& L, float* __restrict__ HYP, float* __restrict__ S0, float* lds, int hb) {
+  constexpr int SR = 8, SP = HYF_SP, HCG = 3, Kq = 48;
+  const int S = d.S, NH = d.NH, n = d.n, E = d.E, NCH = (NH + 63) / 64;
+  const int z = hb & 1, m0 = (hb >> 1) * 32;
+  const float* __restrict__ P = z ? P1 : P0;
+  float* st = lds;                   // [32][SP] gathered states, zero K-padding
+  float* wst = st + 32 * SP;         // [4][HYF_GS] one weight chunk
+  float* bias_s = wst + 4 * HYF_GS;  // [NH]
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c16 = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (wv < 4) {
+    // ---- loader waves (hyper_ws_kernel's fetch / stage)
+    const int lw = wv;
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)P, (short)0, (int)(L.o[MQ_P_COUNT] * sizeof(float)), 0x00020000);
+    const int voff = 4 * lane;
+    float wr[48];
+    auto fetch = [&](int c) {
+      const int j0 = min(16 * (4 * c + lw), NH - 16);
+      const HypSeg sg = hyp_seg(L, n * E, E, j0);
+      const int base = (int)(sg.w + (int64_t)sg.row * S) * 4;
+#pragma unroll
+      for (int q = 0; q < 48; ++q)
+        wr[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(prs, voff, base + 256 * q, 0));
+    };
+    float* const dst = wst + lw * HYF_GS + lane;
+    auto stage = [&]() {
+#pragma unroll
+      for (int q = 0; q < 48; ++q) dst[64 * q] = wr[q];
+    };
+    fetch(0);
+    for (int j = lw * 64 + lane; j < NH; j += 4 * 64) {
+      const HypSeg sg = hyp_seg(L, n * E, E, j);
+      bias_s[j] = P[sg.b + sg.row];
+    }
+    stage();
+    __syncthreads();   // B0: chunk 0, biases and states
+    for (int c = 0; c < NCH; ++c) {
+      if (c + 1 < NCH) fetch(c + 1);   // in flight under chunk c's MFMAs
+      __syncthreads();                 // B1: chunk c consumed
+      if (c + 1 < NCH) stage();
+      __syncthreads();                 // B2: chunk c + 1 staged
+    }
+    return;
+  }
+  // ---- MFMA waves: gather this wave's 8 state rows, then N-tile mw of every chunk for both M-tiles
+  const int mw = wv - 4;
+  {
+    float vs[SR][HCG];
+#pragma unroll
+    for (int i = 0; i < SR; ++i) {
+      const int m = m0 + SR * mw + i, mc = min(m, d.M - 1);
+      const int t = (int)fdiv((uint32_t)mc, d.dB), b = mc - t * d.B;
+      const float* row = rp.state + (rp.ep(b) * d.t_stride + t + z) * (int64_t)S;
+#pragma unroll
+      for (int cg = 0; cg < HCG; ++cg) vs[i][cg] = row[min(lane + 64 * cg, S - 1)];
+    }
+#pragma unroll
+    for (int i = 0; i < SR; ++i) {
+      const int ii = SR * mw + i, m = m0 + ii;
+#pragma unroll
+      for (int cg = 0; cg < HCG; ++cg) {
+        const int col = lane + 64 * cg;
+        const float v = (col < S && m < d.M) ? vs[i][cg] : 0.0f;
+        st[ii * SP + col] = v;
+        if (z == 0 && S0 && m < d.M && col < S) S0[(int64_t)m * S + col] = v;
+      }
+    }
+  }
+  const int ntile = mw;
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(HYP + (int64_t)z * d.M * NH), (short)0, (int)((int64_t)d.M * NH * sizeof(float)), 0x00020000);
+  const float* a0 = st + c16 * SP + g * Kq;
+  const float* a1 = st + (16 + c16) * SP + g * Kq;
+  const float* bw = wst + ntile * HYF_GS + c16 * S + g * Kq;
+  __syncthreads();   // B0
+  for (int c = 0; c < NCH; ++c) {
+    f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+#pragma unroll
+    for (int mm = 0; mm < Kq / 4; ++mm) {
+      const f32x4 bv = *(const f32x4*)&bw[4 * mm];
+      const f32x4 av0 = *(const f32x4*)&a0[4 * mm];
+      const f32x4 av1 = *(const f32x4*)&a1[4 * mm];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc0 = mfma16x4(av0[e], bv[e], acc0);
+        acc1 = mfma16x4(av1[e], bv[e], acc1);
+      }
+    }
+    __syncthreads();   // B1: the loaders may overwrite the chunk
+    if (64 * c + 16 * ntile < NH) {   // wave-uniform: NH % 16 == 0
+      const float bj = bias_s[64 * c + 16 * ntile + c16];
+      const int ob0 = ((m0 + 4 * g) * NH + 16 * ntile + c16) * 4, ob1 = ob0 + 16 * NH * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc0[e] + bj), ors, ob0,
+                                              (e * NH + 64 * c) * 4, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc1[e] + bj), ors, ob1,
+                                              (e * NH + 64 * c) * 4, 0);
+      }
+    }
+    __syncthreads();   // B2
+  }
+}
+
 // VAR: ablation bits for scripts/rec_micro.hip only (production = 0): 1 skip Hs/Gates stores, 2 stamp the T loop,
 // 128 chain waves without priority, 256 gathers two chunks ahead, 512 producer work spread over all 16 phases,
 // 1024 target chain above the online chain,
@@ -69,18 +190,26 @@ struct FusedLds {
 // the gate sums of unit 4 r16 + 2 b3 + b2 = the lane's quad index, the default gate-math layout.
 // NG: obs gather slots per producer thread (16 * O <= 256 * NG); the host picks the smallest instantiation
 // (launch_fwd_fused) because every slot holds two VGPRs across the whole T loop.
-template <int VAR = 0, int NG = FGATHER>
+// HYP = 1: workgroups past the 2R row-nets run hyper_fwd_body (grid 2R + 2 ceil(M / 32), 1-D).
+template <int VAR = 0, int NG = FGATHER, int HYP = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void gru_fwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P0,
                                                                const float* __restrict__ P1, Lay L, Work w) {
   __shared__ FusedLds S;
-  const int z = blockIdx.y;
+  static_assert(sizeof(FusedLds) >= hyf_floats() * sizeof(float), "hypernet workgroups reuse the forward's LDS");
+  // row-net index: (row, net) of a (R, 2) grid, or the 1-D grid's first 2R workgroups (online rows, then target)
+  const int bid = blockIdx.y * gridDim.x + blockIdx.x;
+  if (HYP && bid >= 2 * d.R) {
+    hyper_fwd_body(d, rp, P0, P1, L, w.HYP, w.S0, (float*)&S, bid - 2 * d.R);
+    return;
+  }
+  const int z = bid >= d.R ? 1 : 0;
   const bool online = z == 0;
   const float* __restrict__ P = z ? P1 : P0;
   const int tid = threadIdx.x;
   const bool rec = tid < 256;
   const int R = d.R, Tp = d.Tp, I = d.I, O = d.O, A = d.A, n = d.n;
   const int cl = (Tp - 1) / FCH;   // last chunk
-  const int r = blockIdx.x;
+  const int r = bid - z * R;
   // Output addressing: a wave-uniform base (SGPR pointer) plus a 32-bit per-lane offset, so every global access is
   // one saddr load / store with no 64-bit VALU address math.
   const uint32_t RH = (uint32_t)R * H;
@@ -155,7 +284,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     if (tid < H) S.h0[tid] = 0.0f;   // init_hidden: h0 = 0
   };
   if ((VAR & 64) && tid == 256)
-    ((uint64_t*)w.slab_mix)[16 * (blockIdx.y * gridDim.x + blockIdx.x)] = __builtin_amdgcn_s_memrealtime();
+    ((uint64_t*)w.slab_mix)[16 * bid] = __builtin_amdgcn_s_memrealtime();
 
   if (rec) {
     // ================================================================ recurrence waves
@@ -323,7 +452,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       if (tid == 0) {
 #pragma unroll
         for (int i = 0; i < FCH; ++i)
-          ((uint64_t*)w.slab_mix)[FCH * (blockIdx.y * gridDim.x + blockIdx.x) + i] = bins[i];
+          ((uint64_t*)w.slab_mix)[FCH * bid + i] = bins[i];
       }
     } else {
       for (int t = 0; t < Tp; ++t) step(t);
@@ -331,12 +460,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     __builtin_amdgcn_s_setprio(0);
     if ((VAR & 2048) && tid == 0) {
 #pragma unroll
-      for (int i = 0; i < 5; ++i) ((uint64_t*)w.slab_mix)[16 * (blockIdx.y * gridDim.x + blockIdx.x) + 8 + i] = ph[i];
+      for (int i = 0; i < 5; ++i) ((uint64_t*)w.slab_mix)[16 * bid + 8 + i] = ph[i];
     }
     if ((VAR & 2) && tid == 0) {   // diagnostic only: shader cycles and 100 MHz ticks of the whole T loop
       const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-      ((uint64_t*)w.slab_mix)[2 * (blockIdx.y * gridDim.x + blockIdx.x)] = c1 - c0;
-      ((uint64_t*)w.slab_mix)[2 * (blockIdx.y * gridDim.x + blockIdx.x) + 1] = r1 - r0t;
+      ((uint64_t*)w.slab_mix)[2 * bid] = c1 - c0;
+      ((uint64_t*)w.slab_mix)[2 * bid + 1] = r1 - r0t;
     }
     return;
   }
@@ -462,7 +591,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   };
 
   // chunk 0 synchronously (5 barriers, matched by the recurrence waves)
-  uint64_t* stp = (uint64_t*)w.slab_mix + 16 * (blockIdx.y * gridDim.x + blockIdx.x);
+  uint64_t* stp = (uint64_t*)w.slab_mix + 16 * bid;
   auto stamp = [&](int k) {   // VAR bit 64 (microbenchmark): prologue milestones, 100 MHz ticks
     if ((VAR & 64) && ptid == 0) stp[k] = __builtin_amdgcn_s_memrealtime();
   };
@@ -575,6 +704,15 @@ inline void launch_fwd_fused_v(dim3 grid, hipStream_t s, const Dims& d, const Re
     hipLaunchKernelGGL((gru_fwd_fused_kernel<VAR, 5>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
   else
     hipLaunchKernelGGL((gru_fwd_fused_kernel<VAR, FGATHER>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
+}
+// The production forward with the QMIX hypernet's workgroups appended (HYP = 1; the caller checked hyf_ok).
+inline void launch_fwd_fused_hyp(hipStream_t s, const Dims& d, const Rep& rp, const float* P0, const float* P1,
+                                 const Lay& L, const Work& w) {
+  const dim3 grid(2 * d.R + 2 * ((d.M + 31) / 32));
+  if (FCH * d.O <= 256 * 5)
+    hipLaunchKernelGGL((gru_fwd_fused_kernel<0, 5, 1>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
+  else
+    hipLaunchKernelGGL((gru_fwd_fused_kernel<0, FGATHER, 1>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
 }
 // MQ_FWD_VAR (A/B runs of the schedule variants in the real pipeline, where the obs gather reads cold HBM):
 // 128 chains without priority, 256 gathers two chunks ahead, 512 the rebalanced schedule. Unset = production. Only

@@ -103,6 +103,13 @@ struct mq_handle {
   bool dwh_overlap = getenv("MQ_DWH_OVERLAP") && atoi(getenv("MQ_DWH_OVERLAP")) != 0;
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // QMIX hypernet workgroups appended to the fused forward's grid (gru_fwd_fused.hpp hyper_fwd_body) when the
+  // forward's 2R row-nets exceed two per CU: its second wave leaves CUs idle, and the hypernet fills them
+  // (configs[3]'s shard, R = 320: 0.364 -> 0.346 ms a step). In one wave (cfg2, R = 256) it measured no faster than
+  // hyper_ws_kernel after the forward, which stays. MQ_HYP_IN_FWD=0 never appends, =1 always (A/B switches; the HYP
+  // is bitwise the same either way)
+  int hyp_in_fwd = getenv("MQ_HYP_IN_FWD") ? atoi(getenv("MQ_HYP_IN_FWD")) : -1;
+  int num_cu = 0;
   // A/B switch, off by default: mq_train_step runs reduction pass 2 and the optimiser step as one launch
   // (red_pass2_apply_kernel) unless data parallel. Measured at cfg2 (profiles/r03d_ab_fused_apply): bitwise equal,
   // 13.2-13.5 us against 12.9-13.1 us for the two launches: the ticket hand-off costs what the launch it removes did
@@ -489,11 +496,27 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
   const int rw_bwd = std::min(2, pick_rw(d.R, 256));
   const bool fused_bwd = d.R <= h->fused_bwd_rmax && fused_bwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused_bwd;
   const int rw_fwd = pick_rw(d.R, 512);
+  bool hyp_in_fwd = false;
   if (rw_fwd == 1 && fused_fwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused) {
     plan.fused_fwd = 1;
     // one row per workgroup: fc1 / W_ih / fc2 ride on the recurrence's idle matrix cores (gru_fwd_fused.hpp)
     pt.begin(PH_GRUF);
-    launch_fwd_fused(dim3(d.R, 2), s, d, rp, (const float*)h->on, (const float*)h->tg, L, w);
+    static const bool fwd_var = getenv("MQ_FWD_VAR") != nullptr;
+    if (h->num_cu == 0) {
+      int dev = 0, ncu = 0;
+      h->num_cu = (hipGetDevice(&dev) == hipSuccess &&
+                   hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess) ? ncu : -1;
+    }
+    const bool two_waves = h->num_cu > 0 && d.R > h->num_cu;   // 2R row-nets at two per CU
+    hyp_in_fwd = (h->hyp_in_fwd == 1 || (h->hyp_in_fwd < 0 && two_waves)) && !fwd_var &&
+                 c.mixer == MQ_MIXER_QMIX && !h->force_unfused_mix && hyper_ws_ok(d.S, d.E, d.NH, d.M) &&
+                 hyf_ok(d.S, d.E, d.NH, d.M);
+    if (hyp_in_fwd) {
+      plan.hyper = MQ_HYP_WS;
+      launch_fwd_fused_hyp(s, d, rp, (const float*)h->on, (const float*)h->tg, L, w);
+    } else {
+      launch_fwd_fused(dim3(d.R, 2), s, d, rp, (const float*)h->on, (const float*)h->tg, L, w);
+    }
     MQ_HIP(hipGetLastError());
   } else {
     plan.rw_fwd = rw_fwd;
@@ -523,7 +546,7 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
       MQ_HIP(launch_gemm(p, (int)RT, d.A, 2, s));
     }
   }
-  if (c.mixer == MQ_MIXER_QMIX) {
+  if (c.mixer == MQ_MIXER_QMIX && !hyp_in_fwd) {
     pt.begin(PH_HYP);
     if (hyper_ws_ok(d.S, d.E, d.NH, d.M) && !h->force_unfused_mix) {
       plan.hyper = MQ_HYP_WS;

@@ -516,6 +516,31 @@ def test_fused_pass2_apply_bitwise(cases, name, monkeypatch):
     assert all(np.isfinite(v) for v in outs[0][3].values() if isinstance(v, float))
 
 
+@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg4_qmix", "cfg1_qmix", "tiny_qmix_full", "cfg2_qmix_ragged"])
+def test_hyper_in_forward_grid_bitwise(cases, name, monkeypatch):
+    """The QMIX hypernet as workgroups appended to the fused forward's grid (MQ_HYP_IN_FWD=1; the default for shards
+    past two row-nets per CU, e.g. cfg4) equals hyper_ws_kernel launched after the forward (MQ_HYP_IN_FWD=0) bitwise:
+    parameters, gradients, square_avg and stats over up to four steps, ragged M (cfg1: M = 480, tiny) and the
+    two-wave forward of configs[3]'s shard (cfg4) included."""
+    from tests.gpu_helpers import build, flat_grads, flat_params
+    case = get_case(cases, name)
+    outs = []
+    for inf in ("1", "0"):
+        monkeypatch.setenv("MQ_HYP_IN_FWD", inf)
+        args, buf, mac, learner, logger = build(case)
+        np.random.seed(case.sampler_seed)
+        for k in range(min(4, len(case.episodes))):
+            batch = buf.sample(case.B)
+            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
+        th.cuda.synchronize()
+        assert learner.last_plan()["hyper"] == "ws" and learner.last_plan()["fused_fwd"] == 1
+        outs.append((flat_params(learner), flat_grads(learner), learner._sq.cpu().numpy(), learner.last_stats()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert np.array_equal(outs[0][2], outs[1][2])
+    assert outs[0][3] == outs[1][3]
+
+
 def test_dwh_split_clamped_when_fused(cases, monkeypatch):
     """MQ_DWH_SPLIT above kRedZ = 16: the fused dW_hyper + reduction-pass-1 launch clamps its m-slices to 16 (its
     slabs must go straight to pass 2, never read by pass-1 blocks of the same grid), so the result is bitwise the
