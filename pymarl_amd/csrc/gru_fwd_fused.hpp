@@ -196,20 +196,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                                                                const float* __restrict__ P1, Lay L, Work w) {
   __shared__ FusedLds S;
   static_assert(sizeof(FusedLds) >= hyf_floats() * sizeof(float), "hypernet workgroups reuse the forward's LDS");
-  // row-net index: (row, net) of a (R, 2) grid, or the 1-D grid's first 2R workgroups (online rows, then target)
+  // workgroup index: (row, net) of the (R, 2) grid, or (HYP) the 1-D grid's first 2R workgroups (online rows, then
+  // target) followed by the hypernet's; the HYP = 0 instantiation keeps the 2-D indexing (its register allocation
+  // is the production one)
   const int bid = blockIdx.y * gridDim.x + blockIdx.x;
-  if (HYP && bid >= 2 * d.R) {
-    hyper_fwd_body(d, rp, P0, P1, L, w.HYP, w.S0, (float*)&S, bid - 2 * d.R);
-    return;
+  if constexpr (HYP != 0) {
+    if (bid >= 2 * d.R) {
+      hyper_fwd_body(d, rp, P0, P1, L, w.HYP, w.S0, (float*)&S, bid - 2 * d.R);
+      return;
+    }
   }
-  const int z = bid >= d.R ? 1 : 0;
+  const int z = HYP ? (bid >= d.R ? 1 : 0) : (int)blockIdx.y;
   const bool online = z == 0;
   const float* __restrict__ P = z ? P1 : P0;
   const int tid = threadIdx.x;
   const bool rec = tid < 256;
   const int R = d.R, Tp = d.Tp, I = d.I, O = d.O, A = d.A, n = d.n;
   const int cl = (Tp - 1) / FCH;   // last chunk
-  const int r = bid - z * R;
+  const int r = HYP ? bid - z * R : (int)blockIdx.x;
   // Output addressing: a wave-uniform base (SGPR pointer) plus a 32-bit per-lane offset, so every global access is
   // one saddr load / store with no 64-bit VALU address math.
   const uint32_t RH = (uint32_t)R * H;
