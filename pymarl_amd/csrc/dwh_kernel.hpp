@@ -29,11 +29,13 @@ constexpr int DWH_T = 32;   // output tile edge
 
 // grid = ceil(NH / 32) * ceil((S + 1) / 32) * nsplit (tiles_j = ceil(NH / 32)), 256 threads.
 // VAR (scripts/rec_micro.hip only): 1 no MFMA, 2 no operand loads. U: MFMAs (2 m-rows each) per pipelined block.
+// tid: the thread's index in its 256-thread group; red: that group's [4][DWH_T (DWH_T + 1)] floats of LDS (a
+// 512-thread workgroup runs two tiles, one per half, with one workgroup barrier in common)
 template <int VAR, int U, int NB = 2>
 MQ_DEV void dwh_body(Dims d, Lay L, const float* __restrict__ dHYP, const float* __restrict__ S0,
-                     float* __restrict__ slab, int64_t len, int nsplit, int tiles_j, int lin) {
-  __shared__ float red[4][DWH_T * (DWH_T + 1)];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+                     float* __restrict__ slab, int64_t len, int nsplit, int tiles_j, int lin, int tid, float* red_) {
+  float(*red)[DWH_T * (DWH_T + 1)] = (float(*)[DWH_T * (DWH_T + 1)])red_;
+  const int lane = tid & 63, wv = tid >> 6;
   const int NH = d.NH, S = d.S, M = d.M;
   // 1-D grid, slice-minor: consecutive workgroups go to consecutive XCDs, so with nsplit a multiple of 8 every
   // workgroup of m-slice z runs on XCD z % 8 and the slice's dHYP / S0 rows are fetched into one L2 only
@@ -111,7 +113,8 @@ template <int VAR = 0, int NB = 2>
 __global__ __launch_bounds__(256) void dwh_kernel(Dims d, Lay L, const float* __restrict__ dHYP,
                                                   const float* __restrict__ S0, float* __restrict__ slab,
                                                   int64_t len, int nsplit, int tiles_j) {
-  dwh_body<VAR, 8, NB>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, blockIdx.x);
+  __shared__ float red[4 * DWH_T * (DWH_T + 1)];
+  dwh_body<VAR, 8, NB>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, blockIdx.x, threadIdx.x, red);
 }
 
 // Horizontal fusion: dW_hyper (blocks [0, ndwh)) beside pass 1 of the slab reduction (blocks [ndwh_pad, ..)) in one
@@ -125,7 +128,8 @@ __global__ __launch_bounds__(256) void dwh_red1_kernel(Dims d, Lay L, const floa
                                                        RedPlan pl) {
   const int b = blockIdx.x;
   if (b < ndwh_pad) {
-    if (b < ndwh) dwh_body<0, 8, NB>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, b);
+    __shared__ float red[4 * DWH_T * (DWH_T + 1)];
+    if (b < ndwh) dwh_body<0, 8, NB>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, b, threadIdx.x, red);
     return;
   }
   red_pass1_body(pl, b - ndwh_pad);
@@ -134,7 +138,8 @@ __global__ __launch_bounds__(256) void dwh_red1_kernel(Dims d, Lay L, const floa
 __global__ __launch_bounds__(256, 10) void dwh_side_kernel(
     Dims d, Lay L, const float* __restrict__ dHYP, const float* __restrict__ S0, float* __restrict__ slab, int64_t len,
     int nsplit, int tiles_j) {
-  dwh_body<0, 2>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, blockIdx.x);
+  __shared__ float red[4 * DWH_T * (DWH_T + 1)];
+  dwh_body<0, 2>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, blockIdx.x, threadIdx.x, red);
 }
 
 }  // namespace mq

@@ -21,6 +21,7 @@
 #pragma once
 #include <cstdlib>
 #include "gru_fwd_fused.hpp"
+#include "dwh_kernel.hpp"
 
 namespace mq {
 
@@ -95,11 +96,25 @@ inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_
 // lane (bit 3 of c picks which unit pair stays in A, bit 2 which unit leads each pair), so one row_ror:8 add (pairs
 // c, c ^ 8), one row_half_mirror add (pairs c, 7 - c: bit 2 differs) and the quad sum leave unit 4 r16 + 2 b3 + b2
 // = the lane's own quad index in all four lanes of the quad: the gate-math layout of the default path, unchanged.
-template <int VAR = 0>
+// DWH = 1: workgroups past the R rows compute dW_hyper tiles (dwh_body, two 256-thread tiles per workgroup, tile
+// geometry in w.dwh_*): dispatched after every row, they take the CUs a second wave of rows leaves idle
+// (configs[3]'s shard, R = 320 > 256 CUs) instead of running in the reduction's launch. Same tiles, same m order:
+// bitwise dwh_red1_kernel's slabs.
+template <int VAR = 0, int DWH = 0>
 __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
                                                             Work w, int64_t slab_len, int64_t slab1_len) {
   __shared__ BwdFusedLds S;
   extern __shared__ float dyn[];   // W2 [A][H] | dW2 partial [A][H] | db2 [A]
+  if constexpr (DWH != 0) {
+    static_assert(sizeof(BwdFusedLds) >= 2 * 4 * DWH_T * (DWH_T + 1) * sizeof(float), "dW_hyper tiles reuse the LDS");
+    if ((int)blockIdx.x >= d.R) {
+      const int half = (int)threadIdx.x >> 8;
+      const int lin = min(2 * ((int)blockIdx.x - d.R) + half, w.dwh_n - 1);   // an odd count repeats the last tile
+      dwh_body<0, 8, 4>(d, L, w.dHYP, w.S0, w.slab_mix, w.dwh_len, w.dwh_ns, w.dwh_tj, lin, (int)threadIdx.x & 255,
+                        (float*)&S + half * 4 * DWH_T * (DWH_T + 1));
+      return;
+    }
+  }
   const int tid = threadIdx.x;
   constexpr bool kSplit = (VAR & 1024) != 0;
   constexpr bool kEarlyW2 = (VAR & 2048) != 0;
@@ -708,6 +723,13 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
 // -3.5 us a BPTT against VAR 768 (chain micro 88.8 -> 84.9 us; cfg2 pipeline 0.2277 -> 0.2250 ms a step, r03
 // A/B: profiles/r03_ab_lin_k12.json, teacher-forced parity green at it). MQ_BWD_VAR selects another variant for
 // in-pipeline A/B runs.
+// The production BPTT with dW_hyper's tiles appended (DWH = 1; w.dwh_* set by the caller).
+inline void launch_bwd_fused_dwh(size_t dyn, hipStream_t s, const Dims& d, const Rep& rp, const float* P,
+                                 const Lay& L, const Work& w, int64_t slab_len, int64_t slab1_len) {
+  const dim3 grid(d.R + (w.dwh_n + 1) / 2);
+  hipLaunchKernelGGL((gru_bwd_fused_kernel<768 + 65536 + 16384, 1>), grid, dim3(512), dyn, s, d, rp, P, L, w,
+                     slab_len, slab1_len);
+}
 inline void launch_bwd_fused(dim3 grid, size_t dyn, hipStream_t s, const Dims& d, const Rep& rp, const float* P,
                              const Lay& L, const Work& w, int64_t slab_len, int64_t slab1_len) {
   static const int var = [] { const char* e = std::getenv("MQ_BWD_VAR"); return e ? std::atoi(e) : 768 + 65536 + 16384; }();

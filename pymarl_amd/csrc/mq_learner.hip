@@ -109,6 +109,9 @@ struct mq_handle {
   // hyper_ws_kernel after the forward, which stays. MQ_HYP_IN_FWD=0 never appends, =1 always (A/B switches; the HYP
   // is bitwise the same either way)
   int hyp_in_fwd = getenv("MQ_HYP_IN_FWD") ? atoi(getenv("MQ_HYP_IN_FWD")) : -1;
+  // dW_hyper's tiles appended to the fused BPTT's grid (gru_bwd_fused.hpp, DWH = 1) when its rows exceed the CUs
+  // (a second wave of rows leaves CUs idle); MQ_DWH_IN_BWD=0 never, =1 always (A/B switches; bitwise either way)
+  int dwh_in_bwd = getenv("MQ_DWH_IN_BWD") ? atoi(getenv("MQ_DWH_IN_BWD")) : -1;
   int num_cu = 0;
   // A/B switch, off by default: mq_train_step runs reduction pass 2 and the optimiser step as one launch
   // (red_pass2_apply_kernel) unless data parallel. Measured at cfg2 (profiles/r03d_ab_fused_apply): bitwise equal,
@@ -297,6 +300,15 @@ hipError_t ensure_side(mq_handle* h) {
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
   return e;
+}
+
+int device_cus(mq_handle* h) {
+  if (h->num_cu == 0) {
+    int dev = 0, ncu = 0;
+    h->num_cu = (hipGetDevice(&dev) == hipSuccess &&
+                 hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess) ? ncu : -1;
+  }
+  return h->num_cu;
 }
 
 // dW_hyper: 32 x 32 output tiles x nsplit m-slices, operands straight from global memory (dwh_kernel.hpp)
@@ -502,12 +514,7 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
     // one row per workgroup: fc1 / W_ih / fc2 ride on the recurrence's idle matrix cores (gru_fwd_fused.hpp)
     pt.begin(PH_GRUF);
     static const bool fwd_var = getenv("MQ_FWD_VAR") != nullptr;
-    if (h->num_cu == 0) {
-      int dev = 0, ncu = 0;
-      h->num_cu = (hipGetDevice(&dev) == hipSuccess &&
-                   hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess) ? ncu : -1;
-    }
-    const bool two_waves = h->num_cu > 0 && d.R > h->num_cu;   // 2R row-nets at two per CU
+    const bool two_waves = device_cus(h) > 0 && d.R > h->num_cu;   // 2R row-nets at two per CU
     hyp_in_fwd = (h->hyp_in_fwd == 1 || (h->hyp_in_fwd < 0 && two_waves)) && !fwd_var &&
                  c.mixer == MQ_MIXER_QMIX && !h->force_unfused_mix && hyper_ws_ok(d.S, d.E, d.NH, d.M) &&
                  hyf_ok(d.S, d.E, d.NH, d.M);
@@ -606,6 +613,7 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
     MQ_HIP(launch_dwh(h, d, L, w, s, false));
   }
   pt.begin(PH_GRUB);
+  bool dwh_in_bwd = false;
   plan.fused_bwd = fused_bwd ? 1 : 0;
   plan.rw_bwd = fused_bwd ? 0 : rw_bwd;
   if (fused_bwd) {
@@ -613,7 +621,22 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
     h->nblk_bwd = d.R;
     h->nsplit_fc1 = d.R;
     const size_t dyn = ((size_t)2 * d.A * mq::H + d.A) * sizeof(float);
-    launch_bwd_fused(dim3(d.R), dyn, s, d, rp, (const float*)h->on, L, w, h->len_rnn, (int64_t)mq::H * d.I + mq::H);
+    static const bool bwd_var = getenv("MQ_BWD_VAR") != nullptr;
+    dwh_in_bwd = c.mixer == MQ_MIXER_QMIX && !h->force_unfused_mix && !h->dwh_overlap && !h->dwh_first &&
+                 !h->dwh_unfused && !bwd_var &&
+                 (h->dwh_in_bwd == 1 || (h->dwh_in_bwd < 0 && device_cus(h) > 0 && d.R > h->num_cu));
+    if (dwh_in_bwd) {   // the reduction's dW_hyper blocks, same geometry (see dwh_fused below)
+      w.dwh_tj = (d.NH + DWH_T - 1) / DWH_T;
+      const int ts = (d.S + 1 + DWH_T - 1) / DWH_T;
+      w.dwh_ns = std::max(1, std::min({h->dwh_split, kRedZ, (d.M + 1) / 2}));
+      w.dwh_n = w.dwh_tj * ts * w.dwh_ns;
+      w.dwh_len = h->len_mix;
+      h->nsplit_mix = w.dwh_ns;
+      launch_bwd_fused_dwh(dyn, s, d, rp, (const float*)h->on, L, w, h->len_rnn, (int64_t)mq::H * d.I + mq::H);
+    } else {
+      launch_bwd_fused(dim3(d.R), dyn, s, d, rp, (const float*)h->on, L, w, h->len_rnn,
+                       (int64_t)mq::H * d.I + mq::H);
+    }
     MQ_HIP(hipGetLastError());
   } else {
     {
@@ -647,8 +670,9 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
     }
   }
   // dW_hyper runs fused with pass 1 of the reduction (dwh_red1_kernel) unless an A/B switch placed it elsewhere
-  const bool dwh_fused = c.mixer == MQ_MIXER_QMIX && !side && !dwh_first && !h->force_unfused_mix && !h->dwh_unfused;
-  if (c.mixer == MQ_MIXER_QMIX && !side && !dwh_first && !dwh_fused) {
+  const bool dwh_fused = c.mixer == MQ_MIXER_QMIX && !side && !dwh_first && !h->force_unfused_mix && !h->dwh_unfused &&
+                         !dwh_in_bwd;
+  if (c.mixer == MQ_MIXER_QMIX && !side && !dwh_first && !dwh_fused && !dwh_in_bwd) {
     pt.begin(PH_DWH);
     if (!h->force_unfused_mix) {
       MQ_HIP(launch_dwh(h, d, L, w, s, false));

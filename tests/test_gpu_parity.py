@@ -541,6 +541,30 @@ def test_hyper_in_forward_grid_bitwise(cases, name, monkeypatch):
     assert outs[0][3] == outs[1][3]
 
 
+@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg4_qmix", "cfg1_qmix", "tiny_qmix_full"])
+def test_dwh_in_bptt_grid_bitwise(cases, name, monkeypatch):
+    """dW_hyper's tiles appended to the fused BPTT's grid (MQ_DWH_IN_BWD=1; the default for shards past the CU count,
+    e.g. cfg4) equal dW_hyper in the reduction's launch (MQ_DWH_IN_BWD=0) bitwise: parameters, gradients,
+    square_avg and stats over up to four steps."""
+    from tests.gpu_helpers import build, flat_grads, flat_params
+    case = get_case(cases, name)
+    outs = []
+    for inb in ("1", "0"):
+        monkeypatch.setenv("MQ_DWH_IN_BWD", inb)
+        args, buf, mac, learner, logger = build(case)
+        np.random.seed(case.sampler_seed)
+        for k in range(min(4, len(case.episodes))):
+            batch = buf.sample(case.B)
+            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
+        th.cuda.synchronize()
+        assert learner.last_plan()["fused_bwd"] == 1
+        outs.append((flat_params(learner), flat_grads(learner), learner._sq.cpu().numpy(), learner.last_stats()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert np.array_equal(outs[0][2], outs[1][2])
+    assert outs[0][3] == outs[1][3]
+
+
 def test_dwh_split_clamped_when_fused(cases, monkeypatch):
     """MQ_DWH_SPLIT above kRedZ = 16: the fused dW_hyper + reduction-pass-1 launch clamps its m-slices to 16 (its
     slabs must go straight to pass 2, never read by pass-1 blocks of the same grid), so the result is bitwise the
