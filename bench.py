@@ -9,8 +9,9 @@ under torch.distributed.run a WORLD_SIZE different from --gpus is an error (exit
 
 Metric (BASELINE.json): learner samples/s = B*T*n_agents per train() / wall seconds, whole job (all ranks).
 Default workload = BASELINE configs[1]: QMIX synthetic replay n_agents=8, T=120, obs=80, state=168, batch=32 per
-GPU (weak scaling: every rank trains its own 32-episode shard of one global sample and the ranks all-reduce the
-gradient once per step over RCCL). The replay (5000 episodes, SURVEY.md §8d recipe) lives in HBM; a step is the
+GPU (weak scaling: every rank passes the same global sample of 32·N episodes to QLearner.train, as the reference's
+run loop does, the learner trains its own 32-episode shard and the ranks all-reduce the gradient once per step over
+RCCL). The replay (5000 episodes, SURVEY.md §8d recipe) lives in HBM; a step is the
 full train(): id sampling on the host, fused gather, both unrolls, double-Q, mixer, loss, BPTT, clip, RMSprop,
 the episode-counted target update — nothing skipped.
 
@@ -421,7 +422,9 @@ def coma_bench(a):
     achieved = step_flops / (chain_ms * 1e-3 / T) / 1e12
     value = B * T * n * a.steps / dt
     if rank != 0:
+        from pymarl_amd.learners.dp import SharedComm
         release_handles(learner, mac)
+        SharedComm.free()
         dist.destroy_process_group()
         return
     cpu = None if (a.no_cpu_baseline or world > 1) else coma_cpu_baseline(a.config, data)
@@ -435,7 +438,7 @@ def coma_bench(a):
                    "coma_dp_mode": learner.dp_mode(B)},
         "dist": dist_info(world, learner, "critic replicated on the whole batch, actor sharded: all_reduce(sum) of "
                                           "the agent [grads | sums] buffer once per train"),
-        "roofline": {"bound": "mfma", "kernel": ("coma_chain_kernel (one cooperative launch, T critic steps)"
+        "roofline": {"bound": "mfma", "kernel": ("coma_chain_kernel (one persistent launch, T critic steps)"
                                                  if learner.critic_path() == "chain"
                                                  else "critic step chain (l1 + head + wgrad, x T)"),
                      "critic_path": learner.critic_path(),
@@ -448,6 +451,8 @@ def coma_bench(a):
     print(json.dumps(line), flush=True)
     release_handles(learner, mac)
     if world > 1:
+        from pymarl_amd.learners.dp import SharedComm
+        SharedComm.free()
         dist.destroy_process_group()
 
 
@@ -511,10 +516,10 @@ def main():
 
     def step(k):
         nonlocal episode
+        # run.py:207-219 unchanged: the global sample, truncated to its max filled length, on every rank; the
+        # data-parallel learner trains its own B-episode shard of it (QLearner.train, learners/dp.py)
         gb = buf.sample(B * world)
-        batch = gb.shard(rank, world) if world > 1 else gb
-        batch = batch[:, :batch.max_t_filled()]
-        learner.train(batch, t_env=1000 * k, episode_num=episode)
+        learner.train(gb[:, :gb.max_t_filled()], t_env=1000 * k, episode_num=episode)
         episode += 8   # batch_size_run episodes per outer-loop iteration (run.py:247, qmix_smac.yaml:10)
 
     for k in range(max(1, a.warmup)):
@@ -587,10 +592,19 @@ def main():
         }
         print(json.dumps(line))
     if world > 1:
+        from pymarl_amd.learners.dp import SharedComm
+        release_handles(learner)
+        SharedComm.free()
         dist.destroy_process_group()
 
 
 if __name__ == "__main__":
+    if os.environ.get("MQ_DUMP_MAPS"):
+        # diagnostics: the process's mappings as Python exits (before the C-level exit handlers run), so the frames
+        # of a crash in exit-time teardown can be resolved to library + offset
+        import atexit
+        import shutil
+        atexit.register(lambda: shutil.copyfile("/proc/self/maps", os.environ["MQ_DUMP_MAPS"]))
     main()
     # release the learners' library handles (cycles included) while the HIP runtime — and a profiler's interception
     # layer, when one is loaded — is still up, not from interpreter-exit finalisers (a cfg5 run under rocprofv3

@@ -73,7 +73,7 @@ int mc_critic_forward(const float* critic, const mc_config* cfg, const mq_replay
  * mc_phase_times writes the last step's [prologue, critic chain, actor] ms (synchronises on the events). */
 int mc_set_timing(mc_handle* h, int32_t on);
 int mc_phase_times(mc_handle* h, float* ms /* [3] */);
-/* How the last mc_train_step ran the critic's T steps: 1 = the persistent cooperative chain (one launch; the
+/* How the last mc_train_step ran the critic's T steps: 1 = the persistent critic chain (one launch; the
  * default where the shape fits: B * n_agents <= 80, n_actions <= 32, not data-parallel; MQ_COMA_CHAIN=0 at
  * mc_create turns it off), 0 = three launches per step, -1 = no train step yet. */
 int32_t mc_last_critic_path(const mc_handle* h);

@@ -31,6 +31,8 @@ def _prod(shape):
 
 
 class EpisodeBatch:
+    dp_shard = None   # (rank, world) when this batch is one rank's shard of a global sample (learners/dp.py)
+
     def __init__(self, scheme, groups, batch_size, max_seq_length, data=None, preprocess=None, device="cpu"):
         self.scheme = scheme.copy()
         self.groups = groups
@@ -152,7 +154,11 @@ class EpisodeBatch:
             new_data.episode_data[k] = v[item[0]]
         ret_bs = self._get_num_items(item[0], self.batch_size)
         ret_max_t = self._get_num_items(item[1], self.max_seq_length)
-        return EpisodeBatch(self.scheme, self.groups, ret_bs, ret_max_t, data=new_data, device=self.device)
+        out = EpisodeBatch(self.scheme, self.groups, ret_bs, ret_max_t, data=new_data, device=self.device)
+        # a time slice of a shard is still that shard
+        if self.dp_shard is not None and isinstance(item[0], slice) and item[0] == slice(None):
+            out.dp_shard = self.dp_shard
+        return out
 
     @staticmethod
     def _get_num_items(indexing_item, max_size):
@@ -248,6 +254,7 @@ class SampledBatch(EpisodeBatch):
         new = cls.__new__(cls)
         new.source, new.ep_ids_np, new.t_len = other.source, other.ep_ids_np, int(t_len)
         new._ep_ids_dev = other._ep_ids_dev
+        new.dp_shard = other.dp_shard
         EpisodeBatch.__init__(new, other.source.scheme, other.source.groups, len(other.ep_ids_np), new.t_len,
                               data=SN(transition_data=_LazyGather(new, True), episode_data=_LazyGather(new, False)),
                               preprocess=None, device=other.source.device)
@@ -267,12 +274,17 @@ class SampledBatch(EpisodeBatch):
         return int(self.materialize().max_t_filled())
 
     def shard(self, rank, world):
-        """Contiguous slice [rank*B/world, (rank+1)*B/world) of the episodes (data-parallel learner)."""
+        """Contiguous slice [rank*B/world, (rank+1)*B/world) of the episodes. The data-parallel learners
+        take the GLOBAL sample and call this themselves (learners/dp.py local_shard); the result is tagged so that
+        passing it to a data-parallel train() is an error rather than a second sharding."""
         from ..learners.dp import shard_bounds
         lo, hi = shard_bounds(len(self.ep_ids_np), rank, world)
         if self.dense:
-            return EpisodeBatch.__getitem__(self, slice(lo, hi))
-        return SampledBatch(self.source, self.ep_ids_np[lo:hi], self.t_len)
+            out = EpisodeBatch.__getitem__(self, slice(lo, hi))
+        else:
+            out = SampledBatch(self.source, self.ep_ids_np[lo:hi], self.t_len)
+        out.dp_shard = (rank, world)   # a data-parallel learner rejects it: train() takes the global sample
+        return out
 
     def to(self, device):
         """EpisodeBatch.to (episode_buffer.py:91-96), in place as run.py:214-215 calls it. On the buffer's own device

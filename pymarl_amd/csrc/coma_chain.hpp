@@ -1,7 +1,7 @@
 // Persistent COMA critic chain: every live critic step of one COMALearner.train (coma_learner.py:118-139) in ONE
-// cooperative launch, instead of three launches per step (coma_l1 / coma_head / coma_wgrad).
+// persistent launch, instead of three launches per step (coma_l1 / coma_head / coma_wgrad).
 //
-// G = 8 * NK workgroups of 512 threads, all resident (hipLaunchCooperativeKernel). Workgroup (ut, ks) owns the W1
+// G = 8 * NK workgroups of 512 threads, all resident (G <= the CU count, one per CU). Workgroup (ut, ks) owns the W1
 // tile [16 units ut][CC_KW columns ks] for the whole train: the tile stays in LDS and its RMSprop square_avg and
 // gradient in registers, so W1 (the critic's 111k-element bulk at MMM2) never leaves the CU between steps. The first
 // NHEAD = ceil(R / 16) workgroups also run the head of one 16-row tile. fc1.bias / fc2 / fc3 live in P (the caller's
@@ -741,6 +741,15 @@ __global__ __launch_bounds__(256) void coma_chain_restore_kernel(const int* __re
     P[i] = bak[i];
     SQ[i] = bak[Pc + i];
   }
+}
+
+// Replicated data-parallel critic: the chain's error word travels to every rank in the agent gradient's all-reduce
+// (the spare sum slot 7, 0 on success), and every rank then halts on the sum, so all ranks roll back together.
+__global__ void coma_halt_to_sum_kernel(const int* __restrict__ halt, float* __restrict__ slot) {
+  if (threadIdx.x == 0) *slot = *halt != 0 ? 1.0f : 0.0f;
+}
+__global__ void coma_sum_to_halt_kernel(const float* __restrict__ slot, int* __restrict__ halt) {
+  if (threadIdx.x == 0) *halt = *slot > 0.5f ? 1 : 0;
 }
 
 }  // namespace mq

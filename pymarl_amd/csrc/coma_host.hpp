@@ -389,7 +389,7 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
   bool actor_side = false;
   if (h->timing) MQ_HIP(hipEventRecord(h->ev[1], s));
   bool chained = false;
-  if (!dp && h->chain_env && cc_ok(R, A, h->Kc, h->num_cu)) {   // every critic step in one cooperative launch
+  if (!dp && h->chain_env && cc_ok(R, A, h->Kc, h->num_cu)) {   // every critic step in one persistent launch
     CChain cc;
     cc.d = cd; cc.rp = rp; cc.P = h->critic; cc.SQ = h->csq; cc.G = h->cgrad;
     cc.o_w1 = ca.o_w1; cc.o_b1 = ca.o_b1; cc.o_w2 = ca.o_w2; cc.o_b2 = ca.o_b2; cc.o_w3 = ca.o_w3; cc.o_b3 = ca.o_b3;
@@ -416,17 +416,19 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
     // the chain updates the critic in place: keep the pre-train version, restored below if a hand-off times out
     MQ_HIP(hipMemcpyAsync(h->Pbak, h->critic, (size_t)h->Pc * sizeof(float), hipMemcpyDeviceToDevice, s));
     MQ_HIP(hipMemcpyAsync(h->Pbak + h->Pc, h->csq, (size_t)h->Pc * sizeof(float), hipMemcpyDeviceToDevice, s));
-    void* args[] = {&cc};
-    const hipError_t e = hipLaunchCooperativeKernel((const void*)coma_chain_kernel, dim3(cc.NG), dim3(CC_THREADS),
-                                                    args, (unsigned)lds, s);
+    // A plain launch: the grid (cc_ok: at most one 512-thread workgroup per CU, NG <= the CU count) is resident
+    // by its size alone, which is all a cooperative launch would add a check for (MI355X_MICROARCH.md "Residency
+    // and cooperative launch": plain and cooperative launches give the same residency). Nothing else on the device
+    // waits on the chain, so a workgroup that starts late only delays it; every spin is bounded. The cooperative
+    // launch also cost 15-19 us of host time per train and, under rocprofv3, its dedicated HIP queue crashed the
+    // runtime's exit-time teardown (round 4: profiles/r04a_cfg5_rocprof_exit_crash.txt)
+    hipLaunchKernelGGL(coma_chain_kernel, dim3(cc.NG), dim3(CC_THREADS), lds, s, cc);
+    const hipError_t e = hipGetLastError();
     if (e == hipSuccess) {
       chained = true;
       // failure semantics: after a timed-out hand-off the critic (params, square_avg) is put back to its pre-train
-      // version here and the actor's apply is skipped (its halt word), so the learner state is this train()'s
-      // starting state and COMALearner.train raises
-      hipLaunchKernelGGL(coma_chain_restore_kernel, dim3(64), dim3(256), 0, s, (const int*)h->cstate,
-                         (const float*)h->Pbak, h->critic, h->csq, h->Pc);
-      MQ_HIP(hipGetLastError());
+      // version before the actor's apply (coma_chain_restore_kernel below) and the actor's apply is skipped (its
+      // halt word), so the learner state is this train()'s starting state and COMALearner.train raises
       if (h->chain_trace) {   // debug: per-phase spans of workgroup 0 (100 MHz clock), averaged over <= 16 steps
         unsigned long long hb[16 * 8];
         MQ_HIP(hipMemcpyAsync(hb, h->chain_trace, sizeof(hb), hipMemcpyDeviceToHost, s));
@@ -437,8 +439,7 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
         std::fprintf(stderr, "coma_chain ns/step: A %.0f bar1 %.0f B %.0f bar2 %.0f C %.0f bar3 %.0f D %.0f next %.0f\n",
                      acc[0] / 14, acc[1] / 14, acc[2] / 14, acc[3] / 14, acc[4] / 14, acc[5] / 14, acc[6] / 14, acc[7] / 14);
       }
-    } else {   // the grid cannot be co-resident here: the three-launch path, from now on
-      (void)hipGetLastError();
+    } else {   // the launch was refused: the three-launch path, from now on
       h->chain_env = false;
     }
     // Launched after the chain on a low-priority stream, so the chain's workgroups are normally dispatched first.
@@ -545,11 +546,26 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
     MQ_HIP(hipGetLastError());
     nnorm = rb.b2;
   }
+  if (repl && chained) {   // the chain's error word rides in the agent sums' spare slot 7 (0 on success)
+    hipLaunchKernelGGL(coma_halt_to_sum_kernel, dim3(1), dim3(64), 0, s, (const int*)(h->cstate + 3),
+                       h->agrad + h->Pa + 7);
+    MQ_HIP(hipGetLastError());
+  }
   if (dp || repl) {   // the agent gradient + loss / mask sums, then the norm partials of the summed gradient
     rc = mc_allreduce(h, h->agrad, h->Pa + MQ_NSUMS, s);
     if (rc) return rc;
+    if (repl && chained) {   // any rank's chain failure halts every rank: all roll back, skip the apply and raise
+      hipLaunchKernelGGL(coma_sum_to_halt_kernel, dim3(1), dim3(64), 0, s, (const float*)(h->agrad + h->Pa + 7),
+                         h->cstate + 3);
+      MQ_HIP(hipGetLastError());
+    }
     nnorm = 256;
     hipLaunchKernelGGL(sumsq_kernel, dim3(nnorm), dim3(256), 0, s, (const float*)h->agrad, h->Pa, h->norm_part);
+    MQ_HIP(hipGetLastError());
+  }
+  if (chained) {   // a timed-out chain (on any rank, when replicated): the critic back to its pre-train version
+    hipLaunchKernelGGL(coma_chain_restore_kernel, dim3(64), dim3(256), 0, s, (const int*)h->cstate,
+                       (const float*)h->Pbak, h->critic, h->csq, h->Pc);
     MQ_HIP(hipGetLastError());
   }
   {

@@ -12,13 +12,10 @@
 // tile (coalesced along s) into slab[z] in the parameter layout relative to hyper_w_1.weight. red_pass1 sums the
 // nsplit partials. The m loop is branch-free: rows past the slice read a clamped row with a zero factor.
 //
-// Two instances: dwh_kernel (8 MFMAs per pipelined block, serial after the BPTT) and dwh_side_kernel (2 per block,
-// capped at 48 VGPRs by __launch_bounds__(256, 10); the compiler's warning that LDS holds its occupancy at 6 is
-// expected), which runs on a second stream beside the fused BPTT: the BPTT workgroup (one per CU, 231 -> 232 VGPRs
-// x 2 waves per SIMD, 134 KB + W2 of LDS) leaves 48 VGPRs per SIMD and ~22 KB of LDS free, room for one dwh_side
-// workgroup (17 KB). It fits, and loses: its MFMA waves on the chain's SIMDs slow the BPTT chain by 14 % (cfg2:
-// 92.7 -> 105.6 us, step 238 -> 264 us, r01l A/B), so it is an A/B switch only (MQ_DWH_OVERLAP=1).
-// Each wave walks the same m steps in the same order in both, so their results are bitwise equal.
+// Two hosts of dwh_body: dwh_red1_kernel (beside pass 1 of the slab reduction, the default) and the fused BPTT's
+// appended workgroups (gru_bwd_fused.hpp, DWH = 1). Each wave walks the same m steps in the same order in both, so
+// their results are bitwise equal. (A side-stream instance beside the BPTT lost its A/B in round 1 — its MFMA waves
+// on the chain's SIMDs slowed the BPTT 14 %, profiles/r01m_ab_dwh/ — and was removed in round 4.)
 #pragma once
 #include "learner_gemms.hpp"
 #include "optim_kernels.hpp"
@@ -28,10 +25,10 @@ namespace mq {
 constexpr int DWH_T = 32;   // output tile edge
 
 // grid = ceil(NH / 32) * ceil((S + 1) / 32) * nsplit (tiles_j = ceil(NH / 32)), 256 threads.
-// VAR (scripts/rec_micro.hip only): 1 no MFMA, 2 no operand loads. U: MFMAs (2 m-rows each) per pipelined block.
+// U: MFMAs (2 m-rows each) per pipelined block.
 // tid: the thread's index in its 256-thread group; red: that group's [4][DWH_T (DWH_T + 1)] floats of LDS (a
 // 512-thread workgroup runs two tiles, one per half, with one workgroup barrier in common)
-template <int VAR, int U, int NB = 2>
+template <int U, int NB>
 MQ_DEV void dwh_body(Dims d, Lay L, const float* __restrict__ dHYP, const float* __restrict__ S0,
                      float* __restrict__ slab, int64_t len, int nsplit, int tiles_j, int lin, int tid, float* red_) {
   float(*red)[DWH_T * (DWH_T + 1)] = (float(*)[DWH_T * (DWH_T + 1)])red_;
@@ -61,20 +58,13 @@ MQ_DEV void dwh_body(Dims d, Lay L, const float* __restrict__ dHYP, const float*
       const int m = 2 * stp + half;
       const int mc = min(m, M - 1);
       const float live = (stp < se && m < M) ? 1.0f : 0.0f;
-      if (VAR & 2) {
-        a[u] = amul * (float)mc; b[u] = live;
-      } else {
-        a[u] = fmaf(S0[(int64_t)mc * S + sl], amul, aadd);
-        b[u] = dHYP[(int64_t)mc * NH + jl] * live;
-      }
+      a[u] = fmaf(S0[(int64_t)mc * S + sl], amul, aadd);
+      b[u] = dHYP[(int64_t)mc * NH + jl] * live;
     }
   };
   auto mma = [&](const float (&a)[U], const float (&b)[U]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (VAR & 1) acc[u] = fmaf(a[u], b[u], acc[u]);
-      else acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
-    }
+    for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[u], acc, 0, 0, 0);
   };
   constexpr int BLK = 4 * U;   // steps per block over the four waves
   const int st = sb + wv;
@@ -109,19 +99,11 @@ MQ_DEV void dwh_body(Dims d, Lay L, const float* __restrict__ dHYP, const float*
   }
 }
 
-template <int VAR = 0, int NB = 2>
-__global__ __launch_bounds__(256) void dwh_kernel(Dims d, Lay L, const float* __restrict__ dHYP,
-                                                  const float* __restrict__ S0, float* __restrict__ slab,
-                                                  int64_t len, int nsplit, int tiles_j) {
-  __shared__ float red[4 * DWH_T * (DWH_T + 1)];
-  dwh_body<VAR, 8, NB>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, blockIdx.x, threadIdx.x, red);
-}
-
 // Horizontal fusion: dW_hyper (blocks [0, ndwh)) beside pass 1 of the slab reduction (blocks [ndwh_pad, ..)) in one
 // launch. Neither reads the other's output (pass 1 covers the BPTT's and the mixer's slabs; dW_hyper's own slabs
 // are summed in pass 2, which reads them directly), so the reduction's HBM reads overlap dW_hyper's MFMA chains
 // instead of following them. ndwh_pad is a multiple of 16, so pass 1's block -> XCD mapping is unchanged.
-template <int NB = 2>
+template <int NB = 4>
 __global__ __launch_bounds__(256) void dwh_red1_kernel(Dims d, Lay L, const float* __restrict__ dHYP,
                                                        const float* __restrict__ S0, float* __restrict__ slab,
                                                        int64_t len, int nsplit, int tiles_j, int ndwh, int ndwh_pad,
@@ -129,17 +111,10 @@ __global__ __launch_bounds__(256) void dwh_red1_kernel(Dims d, Lay L, const floa
   const int b = blockIdx.x;
   if (b < ndwh_pad) {
     __shared__ float red[4 * DWH_T * (DWH_T + 1)];
-    if (b < ndwh) dwh_body<0, 8, NB>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, b, threadIdx.x, red);
+    if (b < ndwh) dwh_body<8, NB>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, b, threadIdx.x, red);
     return;
   }
   red_pass1_body(pl, b - ndwh_pad);
-}
-
-__global__ __launch_bounds__(256, 10) void dwh_side_kernel(
-    Dims d, Lay L, const float* __restrict__ dHYP, const float* __restrict__ S0, float* __restrict__ slab, int64_t len,
-    int nsplit, int tiles_j) {
-  __shared__ float red[4 * DWH_T * (DWH_T + 1)];
-  dwh_body<0, 2>(d, L, dHYP, S0, slab, len, nsplit, tiles_j, blockIdx.x, threadIdx.x, red);
 }
 
 }  // namespace mq

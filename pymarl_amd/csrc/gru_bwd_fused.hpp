@@ -35,72 +35,35 @@ struct BwdFusedLds {
   float dx1[FCH][H + 4];     // dX1 of the chunk being reduced
   float db1[4][H];           // fc1 bias-grad partials of the four lane groups
   float wih[G3][H + 1];      // W_ih (dX1's B operand); odd pitch: the four lane groups read rows 48 apart
-  float hnext[H];            // decoupled roles: h of the first step of the chunk processed last (fc2's operand)
-  int cflag[4];              // decoupled roles: per chain wave, the last step whose records it has published
-  int pflag[4];              // decoupled roles: per producer wave, the last chunk it has staged
 };
-
-// Wave-group rendezvous through LDS flags (decoupled roles, VAR 32768): the wave's earlier LDS stores complete
-// (lgkmcnt(0)), lane 0 publishes `cnt` in the wave's flag word, and the wave spins until all four flags of its
-// group reach `cnt`. LDS is one memory per CU and a wave's LDS operations complete in order, so a peer's records
-// are visible once its flag is. Unlike s_barrier it involves only the four waves of one role.
-MQ_DEV void group_sync(volatile int* flags, int wave_in_group, int lane, int cnt) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (lane == 0) flags[wave_in_group] = cnt;
-  // bounded: a wave that never publishes cannot hang the CU (the peers are LDS-local, so a healthy wait is a few
-  // hundred cycles; 2^22 polls is seconds)
-  for (int spins = 0; spins < (1 << 22); ++spins) {
-    const int f0 = flags[0], f1 = flags[1], f2 = flags[2], f3 = flags[3];
-    if (min(min(f0, f1), min(f2, f3)) >= cnt) break;
-  }
-}
 
 inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_fwd_ok(I, O, A, n, RT); }
 
-// VAR: ablation bits (production: see launch_bwd_fused): 4 producers do no MFMA work, 8 per-phase cycle bins of the chain
-// (scripts/rec_micro.hip), 128 chain waves at s_setprio 2, 256 the chain's inputs loaded two steps ahead,
-// 512 the X1 / XIN rows of the next chunk loaded one chunk ahead, 1024 SIMD-split roles: the chain runs in waves
-// 0, 1, 4, 5 and the producers in waves 2, 3, 6, 7. Waves w and w + 4 of a 512-thread workgroup share a SIMD, so
-// the chain then owns two SIMDs outright and the producers' f32 MFMAs (which hold the SIMD's FMA datapath) run on
-// the other two instead of beside every chain wave (measured slower: the producers, two per SIMD, then set the
-// step), 2048 the next step's W2 lookup issued at the top of the step with a 4-slot input rotation, 4096 four
-// accumulator pairs in the W_hh^T mat-vec, 8192 per-phase cycle budget of the chain step (s_memtime stamps of chain
-// wave 0: inputs + gate math + LDS stores | barrier | LDS reads of dgh | W_hh^T FMAs | DPP quad reduction + W2
-// lookup), summed over the steps into w.slab_mix[32 * block + 17 ..] (diagnostic, scripts/chain_micro.hip), 16384
-// the K12 mat-vec layout (below), 32768 decoupled roles (below), 65536 the linearised step (below), 262144 the K12
-// W_hh^T prologue as one dword load per weight (A/B; default: one 16-byte load per row).
-//
-// Linearised step (VAR 65536). Every gate derivative of a step is dh times a coefficient of that step's inputs:
+// The chain step is linearised: every gate derivative of a step is dh times a coefficient of that step's inputs:
 // dn = dh (1 - z), dz = dh (h_{t-1} - n), d(a_n) = dh (1 - z)(1 - n^2), d(a_r) = d(a_n) ghn r (1 - r),
 // d(a_z) = dh (h_{t-1} - n) z (1 - z). So each lane's record value is dh * c (+ h_{t-1} in the h slot) and the
 // carry's own term is dh * z, with c computed from the gate record before dh is known: during the previous step,
 // beside its mat-vec. What stays on the dh chain is dh = carry + dchosen W2[a], two products, the record stores and
-// the mat-vec (the default puts ~15 dependent VALU / DPP operations there: 350 of 1,050 cycles a step measured
-// with the producers idle). Inputs are loaded three steps ahead (four slots). The products are associated
-// differently from the default, so results differ from it by rounding.
+// the mat-vec. Inputs are loaded three steps ahead (four slots). (Round 3: -3.5 us a BPTT against the
+// non-linearised step; profiles/r03_ab_lin_k12.json.)
 //
-// Decoupled roles (VAR 32768). Default: every chain step ends in an s_barrier of all eight waves, so the chain waits
-// for the producer waves whenever a producer phase runs long (measured at cfg2: the barrier is 334 of 1,420 cycles a
-// step with the producers working, 105 with them idle). Decoupled: the four chain waves meet per step through LDS
-// flags (group_sync) and all eight waves meet once per 16-step chunk: at the end of the chain's chunk c the
-// producers have finished chunk c + 1 (its history buffer is then free for chunk c - 1) and start chunk c, whose
-// records are complete. A producer chunk runs its phases back to back (rows staged, one producer-group sync, dW_hh,
-// dW_ih, dX1, dW1, then fc2's 16 steps), in the default order of every accumulation: results are bitwise the
-// default schedule's.
+// K12 layout of the W_hh^T mat-vec: lane c of 16-lane DPP row r16 sums the 12 terms k in [12c, 12c + 12) for the
+// row's four units 4 r16 .. +3 (48 FMAs, as 24 v_pk_fma_f32 with dgh[k] in both halves) and reads only those 12
+// values from LDS (12 KB a step for the four chain waves, against 48 KB for a per-unit layout). The four partial
+// sums per lane are reduce-scattered over the row with no selects: the W pairs are ordered per lane (bit 3 of c
+// picks which unit pair stays in A, bit 2 which unit leads each pair), so one row_ror:8 add (pairs c, c ^ 8), one
+// row_half_mirror add (pairs c, 7 - c: bit 2 differs) and the quad sum leave unit 4 r16 + 2 b3 + b2 = the lane's own
+// quad index in all four lanes of the quad: the lane-split gate-math layout.
 //
-// K12 layout of the W_hh^T mat-vec (VAR 16384). Default: lane (unit k, quarter q) sums 48 of the 192 dgh terms of
-// its own unit, so every chain lane reads 48 dgh values from LDS per step (48 KB a step for the four chain waves).
-// K12: lane c of 16-lane DPP row r16 sums the 12 terms k in [12c, 12c + 12) for the row's four units 4 r16 .. +3
-// (the same 48 FMAs, as 24 v_pk_fma_f32 with dgh[k] in both halves) and reads only those 12 values (12 KB a step).
-// The four partial sums per lane are reduce-scattered over the row with no selects: the W pairs are ordered per
-// lane (bit 3 of c picks which unit pair stays in A, bit 2 which unit leads each pair), so one row_ror:8 add (pairs
-// c, c ^ 8), one row_half_mirror add (pairs c, 7 - c: bit 2 differs) and the quad sum leave unit 4 r16 + 2 b3 + b2
-// = the lane's own quad index in all four lanes of the quad: the gate-math layout of the default path, unchanged.
+// Measured and removed in round 4 (records under profiles/r01*-r03*): decoupled roles meeting through LDS flags,
+// SIMD-split roles, the non-linearised step, four accumulator pairs, the next step's W2 lookup a step early, plain
+// vs non-temporal slab stores, per-weight dword prologue loads; all were slower than this kernel.
+//
 // DWH = 1: workgroups past the R rows compute dW_hyper tiles (dwh_body, two 256-thread tiles per workgroup, tile
 // geometry in w.dwh_*): dispatched after every row, they take the CUs a second wave of rows leaves idle
 // (configs[3]'s shard, R = 320 > 256 CUs) instead of running in the reduction's launch. Same tiles, same m order:
 // bitwise dwh_red1_kernel's slabs.
-template <int VAR = 0, int DWH = 0>
+template <int DWH = 0>
 __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
                                                             Work w, int64_t slab_len, int64_t slab1_len) {
   __shared__ BwdFusedLds S;
@@ -110,22 +73,15 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     if ((int)blockIdx.x >= d.R) {
       const int half = (int)threadIdx.x >> 8;
       const int lin = min(2 * ((int)blockIdx.x - d.R) + half, w.dwh_n - 1);   // an odd count repeats the last tile
-      dwh_body<0, 8, 4>(d, L, w.dHYP, w.S0, w.slab_mix, w.dwh_len, w.dwh_ns, w.dwh_tj, lin, (int)threadIdx.x & 255,
+      dwh_body<8, 4>(d, L, w.dHYP, w.S0, w.slab_mix, w.dwh_len, w.dwh_ns, w.dwh_tj, lin, (int)threadIdx.x & 255,
                         (float*)&S + half * 4 * DWH_T * (DWH_T + 1));
       return;
     }
   }
   const int tid = threadIdx.x;
-  constexpr bool kSplit = (VAR & 1024) != 0;
-  constexpr bool kEarlyW2 = (VAR & 2048) != 0;
-  constexpr bool kAcc4 = (VAR & 4096) != 0;
-  constexpr bool kStamp = (VAR & 8192) != 0;
-  constexpr bool kK12 = (VAR & 16384) != 0;
-  constexpr bool kDec = (VAR & 32768) != 0;
-  constexpr bool kLin = (VAR & 65536) != 0;
-  const bool chain = kSplit ? ((tid >> 7) & 1) == 0 : tid < 256;
+  const bool chain = tid < 256;
   // role-local thread id 0..255 (wave-uniform role; lanes of a quad stay in one wave)
-  const int lt = kSplit ? ((tid & 127) | ((tid >> 8) << 7)) : (tid & 255), k = lt >> 2, q = lt & 3;
+  const int lt = tid & 255, k = lt >> 2, q = lt & 3;
   const int R = d.R, A = d.A, T = d.T, Tp = d.Tp, I = d.I;
   const int cl = (Tp - 1) / FCH;
   const int r = blockIdx.x;
@@ -143,7 +99,6 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       if (tid + 512 * u < A * H) { w2_s[tid + 512 * u] = v[u]; dw2_s[tid + 512 * u] = 0.0f; }
   }
   for (int i = tid; i < A; i += 512) db2_s[i] = 0.0f;
-  if (tid < 4) { S.cflag[tid] = 0; S.pflag[tid] = 0; }
   // zero the history rows past Tp of the top (partial) chunk and the XIN padding
   for (int e = tid; e < 2 * FCH * BRP; e += 512) { (&S.gh[0][0][0])[e] = 0.0f; (&S.gi[0][0][0])[e] = 0.0f; }
   for (int e = tid; e < FCH * FXP; e += 512) (&S.xin[0][0])[e] = 0.0f;
@@ -168,38 +123,24 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
 
   if (chain) {
     // ================================================================ chain waves
-    f32x2 wT[24];   // W_hh[48q .. 48q+47][k] as pairs for v_pk_fma_f32 (K12: see the layout note above)
-    const int c16 = lt & 15;   // K12: lane within the 16-lane DPP row
+    f32x2 wT[24];   // W_hh^T slice as pairs for v_pk_fma_f32 (K12 layout, see above)
+    const int c16 = lt & 15;   // lane within the 16-lane DPP row
     {
       const float* Whh = P + L.o[MQ_P_RNN_W_HH];
-      if (kK12) {
-        const int b3 = (c16 >> 3) & 1, b2 = (c16 >> 2) & 1, u0 = 4 * (lt >> 4);
-        const int a0 = u0 + 2 * b3 + b2, a1 = u0 + 2 * b3 + 1 - b2;               // pair A: the units kept
-        const int v0 = u0 + 2 * (1 - b3) + b2, v1 = u0 + 2 * (1 - b3) + 1 - b2;   // pair B: the partner's
-        if (VAR & 262144) {   // A/B: the round-3 prologue, one dword load per weight
+      const int b3 = (c16 >> 3) & 1, b2 = (c16 >> 2) & 1, u0 = 4 * (lt >> 4);
+      const int a0 = u0 + 2 * b3 + b2, a1 = u0 + 2 * b3 + 1 - b2;               // pair A: the units kept
+      const int v0 = u0 + 2 * (1 - b3) + b2, v1 = u0 + 2 * (1 - b3) + 1 - b2;   // pair B: the partner's
+      // units a0, a1, v0, v1 are u0 .. u0 + 3 in a lane-dependent order: one 16-byte load per row (the compiler
+      // cannot merge the four lane-permuted dword loads itself), then selects
+      auto pick = [](const f32x4& x, int i) { return i == 0 ? x[0] : i == 1 ? x[1] : i == 2 ? x[2] : x[3]; };
+      const int i0 = a0 - u0, i1 = a1 - u0, i2 = v0 - u0, i3 = v1 - u0;
+      f32x4 xr[12];
 #pragma unroll
-          for (int kk = 0; kk < 12; ++kk) {
-            const float* wr = Whh + (12 * c16 + kk) * H;
-            wT[2 * kk] = f32x2{wr[a0], wr[a1]};
-            wT[2 * kk + 1] = f32x2{wr[v0], wr[v1]};
-          }
-        } else {
-          // units a0, a1, v0, v1 are u0 .. u0 + 3 in a lane-dependent order: one 16-byte load per row (the
-          // compiler cannot merge the four lane-permuted dword loads itself), then selects
-          auto pick = [](const f32x4& x, int i) { return i == 0 ? x[0] : i == 1 ? x[1] : i == 2 ? x[2] : x[3]; };
-          const int i0 = a0 - u0, i1 = a1 - u0, i2 = v0 - u0, i3 = v1 - u0;
-          f32x4 xr[12];
+      for (int kk = 0; kk < 12; ++kk) xr[kk] = *(const f32x4*)(Whh + (12 * c16 + kk) * H + u0);
 #pragma unroll
-          for (int kk = 0; kk < 12; ++kk) xr[kk] = *(const f32x4*)(Whh + (12 * c16 + kk) * H + u0);
-#pragma unroll
-          for (int kk = 0; kk < 12; ++kk) {
-            wT[2 * kk] = f32x2{pick(xr[kk], i0), pick(xr[kk], i1)};
-            wT[2 * kk + 1] = f32x2{pick(xr[kk], i2), pick(xr[kk], i3)};
-          }
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < 24; ++c) wT[c] = f32x2{Whh[(48 * q + 2 * c) * H + k], Whh[(48 * q + 2 * c + 1) * H + k]};
+      for (int kk = 0; kk < 12; ++kk) {
+        wT[2 * kk] = f32x2{pick(xr[kk], i0), pick(xr[kk], i1)};
+        wT[2 * kk + 1] = f32x2{pick(xr[kk], i2), pick(xr[kk], i3)};
       }
     }
     // K12 mat-vec on the 12 dgh values of this lane, reduced to the lane's unit (all four lanes of its quad)
@@ -220,9 +161,8 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     // base + idx * stride with per-lane constants, so no lane-dependent branch enters the chain. idx = t except
     // at the edges, clamped with per-lane 0/1 flags: h row 0 stands in for row -1 at t = 0 (hp is zeroed there),
     // dch row T-1 for row T at t = T (dchv is zeroed there). The action is read as the low word of the int64
-    // (little-endian, 0 <= a < A). w2 = W2[a_t][k] is looked up one step ahead (end of the previous step), off
-    // the dh chain.
-    struct In { float g, aux, w2, wd, ci, ch, hq, gz; };   // kLin: wd .. gz are the step's coefficients
+    // (little-endian, 0 <= a < A). w2 = W2[a_t][k] is looked up one step ahead, off the dh chain.
+    struct In { float g, aux, w2, wd, ci, ch, hq, gz; };   // wd .. gz: the step's coefficients
     const float* aux_base;
     int64_t aux_stride;
     if (q == 0) { aux_base = w.Hs + (int64_t)r * H + k - (int64_t)R * H; aux_stride = (int64_t)R * H; }
@@ -231,7 +171,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     const float* g_base = w.Gates + (int64_t)r * (4 * H) + q * H + k;
     const int e0 = q == 0 ? 1 : 0, e12 = (q == 1 || q == 2) ? 1 : 0;
     auto load = [&](int t, In& s) {
-      const int tc = (VAR & 131072) ? T : max(t, 0);   // VAR 131072, diagnostic only: every step loads step T
+      const int tc = max(t, 0);
       const int idx = tc + (e0 & (tc == 0 ? 1 : 0)) - (e12 & (tc >= T ? 1 : 0));
       s.g = g_base[(int64_t)tc * R * (4 * H)];
       s.aux = aux_base[idx * aux_stride];
@@ -241,112 +181,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     const float m0 = q == 0 ? 1.0f : 0.0f, m1 = q == 1 ? 1.0f : 0.0f, m2 = q == 2 ? 1.0f : 0.0f;
     const float m3 = q == 3 ? 1.0f : 0.0f;
     float carry = 0.0f, db_i = 0.0f, db_h = 0.0f;   // bias grads: this lane's component q of b_ih / b_hh
-    uint64_t ph[5] = {0, 0, 0, 0, 0};   // kStamp: cycles per phase, summed over the steps
-    // ahead: the slot whose loads are issued this step (t - 1 with two slots; t - 2 with three, VAR 256, so every
-    // load has two chain steps of latency instead of one); nxt: the next step's slot, whose w2 is looked up here
-    auto step = [&](int t, const In& cur, In& nxt, In& ahead, int dist) {
-      uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0;
-      if (kStamp) s0 = __builtin_amdgcn_s_memtime();
-      load(t - dist, ahead);
-      // VAR 2048: the next step's W2[a][k] lookup is issued here, a whole step before its use, instead of at the
-      // end of the step where its LDS latency sat on the dh chain (nxt was loaded two steps ago: 4-slot rotation)
-      if (kEarlyW2) lookup_w2(nxt);
-      const int p = t & (FCH - 1), cb = (t / FCH) & 1;
-      const float gr = quad_bcast<0>(cur.g), gz = quad_bcast<1>(cur.g), gn = quad_bcast<2>(cur.g),
-                  ghn = quad_bcast<3>(cur.g);
-      const float hp = t > 0 ? quad_bcast<0>(cur.aux) : 0.0f;
-      const float dchv = t < T ? quad_bcast<2>(cur.aux) : 0.0f;
-      const float dh = carry + dchv * cur.w2;
-      const float dn = dh * (1.0f - gz);
-      const float dz = dh * (hp - gn);
-      const float dan = dn * (1.0f - gn * gn);
-      const float dar = (dan * ghn) * (gr * (1.0f - gr));
-      const float daz = dz * (gz * (1.0f - gz));
-      const float rz = fmaf(m0, dar, m1 * daz);
-      const float mine_i = fmaf(m2 + m3, dan, rz);                   // dgi component q (q = 3: unused slot)
-      const float mine_h = fmaf(m2, dan * gr, fmaf(m3, hp, rz));     // dgh component q, or h_{t-1} at q = 3
-      S.gh[cb][p][q * H + k] = mine_h;
-      S.gi[cb][p][q * H + k] = mine_i;
-      db_i = fmaf(1.0f - m3, mine_i, db_i);
-      db_h = fmaf(1.0f - m3, mine_h, db_h);
-      const float cz = dh * gz;
-      if (kStamp) s1 = __builtin_amdgcn_s_memtime();
-      if (kDec) {
-        group_sync(S.cflag, lt >> 6, lt & 63, Tp - t);
-        if (p == 0) lds_barrier();   // end of chunk t / 16: the producers take it (decoupled roles)
-      } else {
-        lds_barrier();
-      }
-      // dh_{t-1} = dh * z + W_hh^T dgh
-      const f32x4* dg4 = (const f32x4*)(&S.gh[cb][p][48 * q]);
-      if (kStamp && kK12) {   // K12 with the LDS reads completed before the FMAs (FMA / reduction split not stamped)
-        s2 = __builtin_amdgcn_s_memtime();
-        const f32x4* d12 = (const f32x4*)(&S.gh[cb][p][12 * c16]);
-        f32x4 dv[3] = {d12[0], d12[1], d12[2]};
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        s3 = __builtin_amdgcn_s_memtime();
-        s4 = s3;
-        carry = cz + k12_sum(dv);
-        lookup_w2(nxt);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const uint64_t s5 = __builtin_amdgcn_s_memtime();
-        ph[0] += s1 - s0; ph[1] += s2 - s1; ph[2] += s3 - s2; ph[3] += s4 - s3; ph[4] += s5 - s4;
-        return;
-      }
-      if (kK12) {
-        const f32x4* d12 = (const f32x4*)(&S.gh[cb][p][12 * c16]);
-        const f32x4 dv[3] = {d12[0], d12[1], d12[2]};
-        carry = cz + k12_sum(dv);
-        if (!kEarlyW2) lookup_w2(nxt);
-        return;
-      }
-      if (kStamp) {   // the same arithmetic as below, with the LDS reads completed before the FMAs
-        s2 = __builtin_amdgcn_s_memtime();
-        f32x4 dv[12];
-#pragma unroll
-        for (int c4 = 0; c4 < 12; ++c4) dv[c4] = dg4[c4];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        s3 = __builtin_amdgcn_s_memtime();
-        f32x2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
-#pragma unroll
-        for (int c4 = 0; c4 < 12; ++c4) {
-          a01 = pk_fma(wT[2 * c4], f32x2{dv[c4][0], dv[c4][1]}, a01);
-          a23 = pk_fma(wT[2 * c4 + 1], f32x2{dv[c4][2], dv[c4][3]}, a23);
-        }
-        const float part = (a01.x + a01.y) + (a23.x + a23.y);
-        asm volatile("" :: "v"(part));
-        s4 = __builtin_amdgcn_s_memtime();
-        carry = cz + quad_sum(part);
-        lookup_w2(nxt);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const uint64_t s5 = __builtin_amdgcn_s_memtime();
-        ph[0] += s1 - s0; ph[1] += s2 - s1; ph[2] += s3 - s2; ph[3] += s4 - s3; ph[4] += s5 - s4;
-        return;
-      }
-      if (kAcc4) {   // VAR 4096: four accumulator pairs, dependency chains of 6 instead of 12
-        f32x2 a0 = {0.0f, 0.0f}, a1 = {0.0f, 0.0f}, a2 = {0.0f, 0.0f}, a3 = {0.0f, 0.0f};
-#pragma unroll
-        for (int c4 = 0; c4 < 12; c4 += 2) {
-          const f32x4 dg = dg4[c4], dh4 = dg4[c4 + 1];
-          a0 = pk_fma(wT[2 * c4], f32x2{dg[0], dg[1]}, a0);
-          a1 = pk_fma(wT[2 * c4 + 1], f32x2{dg[2], dg[3]}, a1);
-          a2 = pk_fma(wT[2 * c4 + 2], f32x2{dh4[0], dh4[1]}, a2);
-          a3 = pk_fma(wT[2 * c4 + 3], f32x2{dh4[2], dh4[3]}, a3);
-        }
-        carry = cz + quad_sum(((a0.x + a0.y) + (a1.x + a1.y)) + ((a2.x + a2.y) + (a3.x + a3.y)));
-      } else {
-        f32x2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
-#pragma unroll
-        for (int c4 = 0; c4 < 12; ++c4) {
-          const f32x4 dg = dg4[c4];
-          a01 = pk_fma(wT[2 * c4], f32x2{dg[0], dg[1]}, a01);
-          a23 = pk_fma(wT[2 * c4 + 1], f32x2{dg[2], dg[3]}, a23);
-        }
-        carry = cz + quad_sum((a01.x + a01.y) + (a23.x + a23.y));
-      }
-      if (!kEarlyW2) lookup_w2(nxt);
-    };
-    // kLin: the step's coefficients (see the note above), computed one step ahead
+    // the step's coefficients (see the note above), computed one step ahead
     auto coeffs = [&](int t, In& s) {
       const float gr = quad_bcast<0>(s.g), gz = quad_bcast<1>(s.g), gn = quad_bcast<2>(s.g), ghn = quad_bcast<3>(s.g);
       const float hp = t > 0 ? quad_bcast<0>(s.aux) : 0.0f;
@@ -371,125 +206,38 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       S.gi[cb][p][q * H + k] = mine_i;
       db_i = fmaf(1.0f - m3, mine_i, db_i);
       db_h = fmaf(1.0f - m3, mine_h, db_h);
-      if (kDec) {
-        group_sync(S.cflag, lt >> 6, lt & 63, Tp - t);
-        if (p == 0) lds_barrier();
-      } else {
-        lds_barrier();
-      }
-      float part;
-      if (kK12) {
-        const f32x4* d12 = (const f32x4*)(&S.gh[cb][p][12 * c16]);
-        const f32x4 dv[3] = {d12[0], d12[1], d12[2]};
-        lookup_w2(nxt);   // the next step's W2[a][k] and coefficients, beside this step's LDS reads and FMAs
-        coeffs(t - 1, nxt);
-        carry = fmaf(dh, cur.gz, k12_sum(dv));
-        return;
-      }
-      const f32x4* dg4 = (const f32x4*)(&S.gh[cb][p][48 * q]);
-      f32x2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
-#pragma unroll
-      for (int c4 = 0; c4 < 12; ++c4) {
-        const f32x4 dg = dg4[c4];
-        a01 = pk_fma(wT[2 * c4], f32x2{dg[0], dg[1]}, a01);
-        a23 = pk_fma(wT[2 * c4 + 1], f32x2{dg[2], dg[3]}, a23);
-      }
-      lookup_w2(nxt);
+      lds_barrier();
+      // dh_{t-1} = dh * z + W_hh^T dgh
+      const f32x4* d12 = (const f32x4*)(&S.gh[cb][p][12 * c16]);
+      const f32x4 dv[3] = {d12[0], d12[1], d12[2]};
+      lookup_w2(nxt);   // the next step's W2[a][k] and coefficients, beside this step's LDS reads and FMAs
       coeffs(t - 1, nxt);
-      part = (a01.x + a01.y) + (a23.x + a23.y);
-      carry = fmaf(dh, cur.gz, quad_sum(part));
+      carry = fmaf(dh, cur.gz, k12_sum(dv));
     };
     In sa, sb, sc, sd;
-    if (kLin) {
-      load(Tp - 1, sa);
-      load(Tp - 2, sb);
-      load(Tp - 3, sc);
-      drain_vmem();
-      lds_barrier();
-      lookup_w2(sa);
-      coeffs(Tp - 1, sa);
-      int t = Tp - 1;
-      for (; t - 3 >= 0; t -= 4) {
-        lstep(t, sa, sb, sd);
-        lstep(t - 1, sb, sc, sa);
-        lstep(t - 2, sc, sd, sb);
-        lstep(t - 3, sd, sa, sc);
-      }
-      if (t >= 0) lstep(t, sa, sb, sd);
-      if (t - 1 >= 0) lstep(t - 1, sb, sc, sa);
-      if (t - 2 >= 0) lstep(t - 2, sc, sd, sb);
-    } else {
     load(Tp - 1, sa);
-    if (VAR & (256 | 2048)) load(Tp - 2, sb);
-    if (kEarlyW2) load(Tp - 3, sc);
+    load(Tp - 2, sb);
+    load(Tp - 3, sc);
     drain_vmem();
     lds_barrier();
     lookup_w2(sa);
+    coeffs(Tp - 1, sa);
     int t = Tp - 1;
-    if (VAR & 128) __builtin_amdgcn_s_setprio(2);
-    if (VAR & 8) {   // diagnostic only: chain cycles per step, binned by the producer phase u = 15 - (t & 15)
-      uint64_t bins[FCH];
-#pragma unroll
-      for (int i = 0; i < FCH; ++i) bins[i] = 0;
-      const uint64_t c0 = __builtin_amdgcn_s_memtime();
-      for (; t >= 0; t -= 2) {
-        const uint64_t a0 = __builtin_amdgcn_s_memtime();
-        step(t, sa, sb, sb, 1);
-        const uint64_t a1 = __builtin_amdgcn_s_memtime();
-        if (t - 1 >= 0) step(t - 1, sb, sa, sa, 1);
-        const uint64_t a2 = __builtin_amdgcn_s_memtime();
-#pragma unroll
-        for (int i = 0; i < FCH; ++i) {
-          if (i == FCH - 1 - (t & (FCH - 1))) bins[i] += a1 - a0;
-          if (t - 1 >= 0 && i == FCH - 1 - ((t - 1) & (FCH - 1))) bins[i] += a2 - a1;
-        }
-      }
-      if (tid == 0) {
-        uint64_t* st = (uint64_t*)w.slab_mix + 32 * blockIdx.x;
-#pragma unroll
-        for (int i = 0; i < FCH; ++i) st[i] = bins[i];
-        st[16] = __builtin_amdgcn_s_memtime() - c0;
-      }
-    } else if (kEarlyW2) {   // 4-slot rotation: inputs loaded three steps ahead
-      for (; t - 3 >= 0; t -= 4) {
-        step(t, sa, sb, sd, 3);
-        step(t - 1, sb, sc, sa, 3);
-        step(t - 2, sc, sd, sb, 3);
-        step(t - 3, sd, sa, sc, 3);
-      }
-      if (t >= 0) step(t, sa, sb, sd, 3);
-      if (t - 1 >= 0) step(t - 1, sb, sc, sa, 3);
-      if (t - 2 >= 0) step(t - 2, sc, sd, sb, 3);
-    } else if (VAR & 256) {
-      for (; t - 2 >= 0; t -= 3) {
-        step(t, sa, sb, sc, 2);
-        step(t - 1, sb, sc, sa, 2);
-        step(t - 2, sc, sa, sb, 2);
-      }
-      if (t >= 0) step(t, sa, sb, sc, 2);
-      if (t - 1 >= 0) step(t - 1, sb, sc, sa, 2);
-    } else {
-      for (; t - 1 >= 0; t -= 2) {
-        step(t, sa, sb, sb, 1);
-        step(t - 1, sb, sa, sa, 1);
-      }
-      if (t >= 0) step(t, sa, sb, sb, 1);
+    for (; t - 3 >= 0; t -= 4) {
+      lstep(t, sa, sb, sd);
+      lstep(t - 1, sb, sc, sa);
+      lstep(t - 2, sc, sd, sb);
+      lstep(t - 3, sd, sa, sc);
     }
-    }   // !kLin
-    if (VAR & 128) __builtin_amdgcn_s_setprio(0);
-    if (kStamp && tid == 0) {
-      uint64_t* st = (uint64_t*)w.slab_mix + 32 * blockIdx.x;
-#pragma unroll
-      for (int i = 0; i < 5; ++i) st[17 + i] = ph[i];
-    }
-    if (!kDec) {
-      lds_barrier();   // producer tail: chunk 0 (2 barriers)
-      lds_barrier();
-    }
+    if (t >= 0) lstep(t, sa, sb, sd);
+    if (t - 1 >= 0) lstep(t - 1, sb, sc, sa);
+    if (t - 2 >= 0) lstep(t - 2, sc, sd, sb);
+    lds_barrier();   // producer tail: chunk 0 (2 barriers)
+    lds_barrier();
     if (q < 3) { slab[o_bi + q * H + k] = db_i; slab[o_bh + q * H + k] = db_h; }
   } else {
     // ================================================================== producer waves
-    const int ptid = kSplit ? lt : tid - 256, wv = ptid >> 6, lane = ptid & 63, g = lane >> 4, c16 = lane & 15;
+    const int ptid = tid - 256, wv = ptid >> 6, lane = ptid & 63, g = lane >> 4, c16 = lane & 15;
     const int Kq = (I + 15) / 16 * 4;
     f32x4 acc_hh[3][4], acc_ih[3][4], acc_w1[7];
 #pragma unroll
@@ -589,8 +337,6 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       }
     };
     // fc2 grads of step t: dW2[a][k] += dchosen * h_t[k]; (a, k) owned by lane (k, q = a % 4); h_t was the
-    // h_{t-1} record of step t+1
-    // fc2 grads of step t: dW2[a][k] += dchosen * h_t[k]; (a, k) owned by lane (k, q = a % 4); h_t was the
     // h_{t-1} record of step t+1. dchosen_t and a_t are wave-uniform loads issued one step ahead.
     float h_next = 0.0f, dch_n = 0.0f;
     int act_n = 0;
@@ -612,46 +358,11 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     };
     fc2_fetch(Tp - 1);
 
-    if (kDec) {
-      // fc2 grads of chunk c's steps, t descending (the default order): dW2[a][k] += dchosen h_t[k], h_t being the
-      // h_{t-1} record of step t + 1 (the next row of this chunk, or S.hnext for its last step)
-      auto fc2_chunk = [&](int c) {
-        const int cb = c & 1, t0 = FCH * c;
-#pragma unroll
-        for (int p = FCH - 1; p >= 0; --p) {
-          const int t = t0 + p;
-          if (t >= T) continue;
-          const float hn = p < FCH - 1 ? S.gh[cb][p + 1][3 * H + k] : S.hnext[k];
-          const float dchv = w.dch[(int64_t)t * R + r];
-          const int a = *(const int*)(arow + (int64_t)t * d.n);
-          if ((a & 3) == q) {
-            dw2_s[a * H + k] += dchv * hn;
-            if (k == 0) db2_s[a] += dchv;
-          }
-        }
-        if (q == 0) S.hnext[k] = S.gh[cb][0][3 * H + k];   // h_{16c - 1}: read by chunk c - 1's last step
-      };
-      lds_barrier();   // prologue (matches the chain's)
-      issue_rows(cl);
-      for (int c = cl; c >= 0; --c) {
-        lds_barrier();   // the chain has published chunk c; this group has finished chunk c + 1
-        store_rows(c);
-        group_sync(S.pflag, wv, lane, cl + 1 - c);   // chunk c's X1 / XIN rows staged by all producer waves
-        if (c > 0) issue_rows(c - 1);
-        if (VAR & 4) continue;   // diagnostic: producers idle
-        dw_rec(c, 0, 4, false);
-        dw_rec(c, 0, 4, true);
-        dx1_part(c, 0, 12);
-        dx1_epi();
-        dw1_part(0, 4);
-        fc2_chunk(c);
-      }
-    } else {
     lds_barrier();
     for (int c = cl; c >= 0; --c) {
       const int C = c + 1;
-      const bool work = !(VAR & 4) && C <= cl;
-      if ((VAR & 512) && c == cl) issue_rows(cl);   // VAR 512: rows one chunk ahead (the top chunk's up front)
+      const bool work = C <= cl;
+      if (c == cl) issue_rows(cl);   // the X1 / XIN rows one chunk ahead (the top chunk's up front)
 #pragma unroll
       for (int u = 0; u < FCH; ++u) {
         const int t = FCH * c + FCH - 1 - u;
@@ -659,7 +370,6 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
         lds_barrier();   // step t's records published
         fc2_grads(t);
         if (work) {
-          if (u == 0 && !(VAR & 512)) issue_rows(C);
           if (u >= 1 && u <= 4) dw_rec(C, u - 1, u, false);
           if (u == 4) store_rows(C);
           if (u >= 5 && u <= 8) dw_rec(C, u - 5, u - 4, true);
@@ -669,25 +379,19 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
           if (u == 14) dw1_part(1, 2);
           if (u == 15) dw1_part(2, 4);
         }
-        if ((VAR & 512) && u == 5 && c < cl) issue_rows(c);   // stored at u = 4 of the next chunk
+        if (u == 5 && c < cl) issue_rows(c);   // stored at u = 4 of the next chunk
       }
     }
     // tail: chunk 0 (2 barriers, matched by the chain waves)
-    if (!(VAR & 4)) {
-      if (!(VAR & 512)) issue_rows(0);
-      dw_rec(0, 0, 4, false);
-      drain_vmem();
-      store_rows(0);
-    }
+    dw_rec(0, 0, 4, false);
+    drain_vmem();
+    store_rows(0);
     lds_barrier();
-    if (!(VAR & 4)) {
-      dw_rec(0, 0, 4, true);
-      dx1_part(0, 0, 12);
-      dx1_epi();
-    }
+    dw_rec(0, 0, 4, true);
+    dx1_part(0, 0, 12);
+    dx1_epi();
     lds_barrier();
-    if (!(VAR & 4)) dw1_part(0, 4);
-    }   // !kDec
+    dw1_part(0, 4);
 
     // per-workgroup slabs in the MFMA C layout: element (16 tile + 4 g + e, 16 tile' + c16)
 #pragma unroll
@@ -718,58 +422,15 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
         (S.db1[0][tid] + S.db1[1][tid]) + (S.db1[2][tid] + S.db1[3][tid]);
 }
 
-// Host: production is VAR 82688 = 512 (X1 / XIN rows one chunk ahead: -0.7 us, r01k A/B) + 256 (unused by the
-// linearised step, which loads its inputs three steps ahead) + 65536 (linearised step) + 16384 (K12 mat-vec):
-// -3.5 us a BPTT against VAR 768 (chain micro 88.8 -> 84.9 us; cfg2 pipeline 0.2277 -> 0.2250 ms a step, r03
-// A/B: profiles/r03_ab_lin_k12.json, teacher-forced parity green at it). MQ_BWD_VAR selects another variant for
-// in-pipeline A/B runs.
-// The production BPTT with dW_hyper's tiles appended (DWH = 1; w.dwh_* set by the caller).
+// Host: the fused BPTT, with dW_hyper's tiles appended (DWH = 1; w.dwh_* set by the caller) or without.
 inline void launch_bwd_fused_dwh(size_t dyn, hipStream_t s, const Dims& d, const Rep& rp, const float* P,
                                  const Lay& L, const Work& w, int64_t slab_len, int64_t slab1_len) {
   const dim3 grid(d.R + (w.dwh_n + 1) / 2);
-  hipLaunchKernelGGL((gru_bwd_fused_kernel<768 + 65536 + 16384, 1>), grid, dim3(512), dyn, s, d, rp, P, L, w,
-                     slab_len, slab1_len);
+  hipLaunchKernelGGL((gru_bwd_fused_kernel<1>), grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
 }
 inline void launch_bwd_fused(dim3 grid, size_t dyn, hipStream_t s, const Dims& d, const Rep& rp, const float* P,
                              const Lay& L, const Work& w, int64_t slab_len, int64_t slab1_len) {
-  static const int var = [] { const char* e = std::getenv("MQ_BWD_VAR"); return e ? std::atoi(e) : 768 + 65536 + 16384; }();
-  if (var == 256)
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<256>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
-  else if (var == 128)
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<128>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
-  else if (var == 768)
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<768>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
-  else if (var == 384)
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<384>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
-  else if (var == 1792)
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<1792>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
-  else if (var == 2816)
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<2816>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
-  else if (var == 4864)
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<4864>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
-  else if (var == 6912)
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<6912>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
-  else if (var == 768 + 32768)   // decoupled roles
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 32768>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
-  else if (var == 768 + 32768 + 16384)   // decoupled roles + K12
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 32768 + 16384>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len,
-                       slab1_len);
-  else if (var == 768 + 65536)   // linearised step
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 65536>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
-  else if (var == 768 + 65536 + 16384 + 262144)   // production with dword W_hh^T prologue loads (A/B)
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 65536 + 16384 + 262144>, grid, dim3(512), dyn, s, d, rp, P, L, w,
-                       slab_len, slab1_len);
-  else if (var == 768 + 65536 + 16384)   // linearised step + K12
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 65536 + 16384>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len,
-                       slab1_len);
-  else if (var == 768 + 16384)   // K12 mat-vec layout
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<768 + 16384>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
-  else if (var == 772)   // diagnostic (wrong gradients): producers idle, the chain alone
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<772>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
-  else if (var == 1796)  // diagnostic (wrong gradients): SIMD-split chain alone
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<1796>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
-  else
-    hipLaunchKernelGGL(gru_bwd_fused_kernel<0>, grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  hipLaunchKernelGGL((gru_bwd_fused_kernel<0>), grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
 }
 
 }  // namespace mq

@@ -177,21 +177,13 @@ MQ_DEV void hyper_fwd_body(const Dims& d, const Rep& rp, const float* __restrict
   }
 }
 
-// VAR: ablation bits for scripts/rec_micro.hip only (production = 0): 1 skip Hs/Gates stores, 2 stamp the T loop,
-// 128 chain waves without priority, 256 gathers two chunks ahead, 512 producer work spread over all 16 phases,
-// 1024 target chain above the online chain,
-// 4 producers idle (recurrence alone on stale gates), 8 per-phase cycle bins, 16 no obs loads, 32 no X1/XIN stores,
-// 64 prologue milestone stamps, 2048 per-phase cycle budget of the chain step (s_memtime stamps of wave 0: LDS reads
-// of h_{t-1} and the input gate | W_hh FMAs | DPP quad reductions | gate math + stores | barrier), summed over the
-// steps into w.slab_mix[16 * block + 8 ..] (diagnostic, scripts/chain_micro.hip), 4096 the K4 mat-vec layout:
-// lane c of 16-lane DPP row r16 sums k in [4c, 4c + 4) for the three gates of the row's four units (the same 48
-// FMAs) and reads one b128 of h_{t-1} instead of four; the twelve partials are reduce-scattered over the row exactly
-// as gru_bwd_fused.hpp's K12 layout does (row_ror:8, row_half_mirror, quad sum, W pairs ordered per lane), leaving
-// the gate sums of unit 4 r16 + 2 b3 + b2 = the lane's quad index, the default gate-math layout.
+// Measured and removed in round 4 (records under profiles/r01*-r03*): the K4 mat-vec layout, chains without
+// priority or with the target chain above the online one, gathers two chunks ahead, producer work spread over all 16
+// phases; each was slower in the cfg2 pipeline.
 // NG: obs gather slots per producer thread (16 * O <= 256 * NG); the host picks the smallest instantiation
 // (launch_fwd_fused) because every slot holds two VGPRs across the whole T loop.
 // HYP = 1: workgroups past the 2R row-nets run hyper_fwd_body (grid 2R + 2 ceil(M / 32), 1-D).
-template <int VAR = 0, int NG = FGATHER, int HYP = 0>
+template <int NG = FGATHER, int HYP = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void gru_fwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P0,
                                                                const float* __restrict__ P1, Lay L, Work w) {
   __shared__ FusedLds S;
@@ -249,7 +241,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const int lim = (Tp - 1 - t0) * nO + O - 1;   // last valid element offset of this chunk
 #pragma unroll
     for (int s = 0; s < NG; ++s)
-      xr[s] = (VAR & 16) ? (float)s : ld_u32(base, (uint32_t)min(opaque(gsl[s]) & 0xFFFFF, lim));
+      xr[s] = ld_u32(base, (uint32_t)min(opaque(gsl[s]) & 0xFFFFF, lim));
     {
       const int t = min(max(t0 + (ptid & (FCH - 1)), 1), Tp - 1) - 1;
       f_ld = *(const int*)(rp.filled + slot0 + t);
@@ -287,60 +279,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     for (int e = tid; e < FCH * FXP; e += 512) (&S.xin[0][0])[e] = 0.0f;
     if (tid < H) S.h0[tid] = 0.0f;   // init_hidden: h0 = 0
   };
-  if ((VAR & 64) && tid == 256)
-    ((uint64_t*)w.slab_mix)[16 * bid] = __builtin_amdgcn_s_memrealtime();
 
   if (rec) {
     // ================================================================ recurrence waves
     const int j = tid >> 2, q = tid & 3;
-    constexpr bool kK4 = (VAR & 4096) != 0;
-    const int c16 = tid & 15;   // K4: lane within the 16-lane DPP row
-    f32x2 wr[8], wz[8], wn[8];   // W_hh[gate * 64 + j][16 q .. 16 q + 15] as pairs for v_pk_fma_f32 (K4: see above)
+    f32x2 wr[8], wz[8], wn[8];   // W_hh[gate * 64 + j][16 q .. 16 q + 15] as pairs for v_pk_fma_f32
     shared_load();
     {
       const float* Whh = P + L.o[MQ_P_RNN_W_HH];
-      if (kK4) {   // [2 kk] = pair A (units kept), [2 kk + 1] = pair B (the partner's), k = 4 c16 + kk
-        const int b3 = (c16 >> 3) & 1, b2 = (c16 >> 2) & 1, u0 = 4 * (tid >> 4);
-        const int a0 = u0 + 2 * b3 + b2, a1 = u0 + 2 * b3 + 1 - b2;
-        const int v0 = u0 + 2 * (1 - b3) + b2, v1 = u0 + 2 * (1 - b3) + 1 - b2;
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const int k = 4 * c16 + kk;
-          wr[2 * kk] = f32x2{Whh[(0 * H + a0) * H + k], Whh[(0 * H + a1) * H + k]};
-          wr[2 * kk + 1] = f32x2{Whh[(0 * H + v0) * H + k], Whh[(0 * H + v1) * H + k]};
-          wz[2 * kk] = f32x2{Whh[(1 * H + a0) * H + k], Whh[(1 * H + a1) * H + k]};
-          wz[2 * kk + 1] = f32x2{Whh[(1 * H + v0) * H + k], Whh[(1 * H + v1) * H + k]};
-          wn[2 * kk] = f32x2{Whh[(2 * H + a0) * H + k], Whh[(2 * H + a1) * H + k]};
-          wn[2 * kk + 1] = f32x2{Whh[(2 * H + v0) * H + k], Whh[(2 * H + v1) * H + k]};
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          wr[k] = f32x2{Whh[(0 * H + j) * H + 16 * q + 2 * k], Whh[(0 * H + j) * H + 16 * q + 2 * k + 1]};
-          wz[k] = f32x2{Whh[(1 * H + j) * H + 16 * q + 2 * k], Whh[(1 * H + j) * H + 16 * q + 2 * k + 1]};
-          wn[k] = f32x2{Whh[(2 * H + j) * H + 16 * q + 2 * k], Whh[(2 * H + j) * H + 16 * q + 2 * k + 1]};
-        }
+      for (int k = 0; k < 8; ++k) {
+        wr[k] = f32x2{Whh[(0 * H + j) * H + 16 * q + 2 * k], Whh[(0 * H + j) * H + 16 * q + 2 * k + 1]};
+        wz[k] = f32x2{Whh[(1 * H + j) * H + 16 * q + 2 * k], Whh[(1 * H + j) * H + 16 * q + 2 * k + 1]};
+        wn[k] = f32x2{Whh[(2 * H + j) * H + 16 * q + 2 * k], Whh[(2 * H + j) * H + 16 * q + 2 * k + 1]};
       }
     }
-    // K4 mat-vec: 4 h values -> this lane's unit's three gate sums (every lane of the quad)
-    auto k4_sums = [&](const f32x4 hv, float& sr, float& sz, float& sn) {
-      f32x2 rA = {0.0f, 0.0f}, rB = {0.0f, 0.0f}, zA = {0.0f, 0.0f}, zB = {0.0f, 0.0f}, nA = {0.0f, 0.0f},
-            nB = {0.0f, 0.0f};
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const f32x2 hh = {hv[kk], hv[kk]};
-        rA = pk_fma(wr[2 * kk], hh, rA); rB = pk_fma(wr[2 * kk + 1], hh, rB);
-        zA = pk_fma(wz[2 * kk], hh, zA); zB = pk_fma(wz[2 * kk + 1], hh, zB);
-        nA = pk_fma(wn[2 * kk], hh, nA); nB = pk_fma(wn[2 * kk + 1], hh, nB);
-      }
-      auto red = [](f32x2 a, f32x2 b) {
-        const float x = a.x + row_ror8(b.x), y = a.y + row_ror8(b.y);
-        return quad_sum(x + row_half_mirror(y));
-      };
-      sr = red(rA, rB);
-      sz = red(zA, zB);
-      sn = red(nA, nB);
-    };
     const float bhr = P[L.o[MQ_P_RNN_B_HH] + j], bhz = P[L.o[MQ_P_RNN_B_HH] + H + j],
                 bhn = P[L.o[MQ_P_RNN_B_HH] + 2 * H + j];
     shared_store();
@@ -354,50 +307,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const float bsel = m0 * bhr + m1 * bhz;
     float hprev = 0.0f;   // h_{t-1}[j]: every lane of the quad computes unit j's h, so it never re-reads LDS
     const uint32_t hlo = q == 0 ? ((uint32_t)r * H + j) * 4 : kDrop, glo = ((uint32_t)r * (4 * H) + q * H + j) * 4;
-    uint64_t ph[5] = {0, 0, 0, 0, 0};
     auto step = [&](int t) {
       const int p = t & (FCH - 1), c = t / FCH;
       const float* hb = t == 0 ? S.h0 : S.hs[((t - 1) / FCH) & 1][(t - 1) & (FCH - 1)];
-      uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0;
-      if (VAR & 2048) s0 = __builtin_amdgcn_s_memtime();
       const float own = S.gi[c & 1][p][gcol];   // issued with the h reads below (same LDS latency window)
       float sr, sz, sn;
-      if (kK4) {
-        const f32x4 hv = *(const f32x4*)(&hb[4 * c16]);
-        if (VAR & 2048) {
-          asm volatile("s_waitcnt lgkmcnt(0)" :: "v"(own), "v"(hv) : "memory");
-          s1 = __builtin_amdgcn_s_memtime();
-          s2 = s1;
-        }
-        k4_sums(hv, sr, sz, sn);
-        if (VAR & 2048) {
-          asm volatile("" :: "v"(sr), "v"(sz), "v"(sn));
-          s3 = __builtin_amdgcn_s_memtime();
-        }
-      } else if (VAR & 2048) {   // the same arithmetic with the LDS reads completed first
-        const f32x4* hv4 = (const f32x4*)(&hb[16 * q]);
-        f32x4 hv[4];
-#pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4) hv[k4] = hv4[k4];
-        asm volatile("s_waitcnt lgkmcnt(0)" :: "v"(own) : "memory");
-        s1 = __builtin_amdgcn_s_memtime();
-        f32x2 ar = {0.0f, 0.0f}, az = {0.0f, 0.0f}, an = {0.0f, 0.0f};
-#pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4) {
-          const f32x2 h01 = {hv[k4][0], hv[k4][1]}, h23 = {hv[k4][2], hv[k4][3]};
-          ar = pk_fma(wr[2 * k4], h01, ar); ar = pk_fma(wr[2 * k4 + 1], h23, ar);
-          az = pk_fma(wz[2 * k4], h01, az); az = pk_fma(wz[2 * k4 + 1], h23, az);
-          an = pk_fma(wn[2 * k4], h01, an); an = pk_fma(wn[2 * k4 + 1], h23, an);
-        }
-        const float pr = ar.x + ar.y, pz = az.x + az.y, pn = an.x + an.y;
-        asm volatile("" :: "v"(pr), "v"(pz), "v"(pn));
-        s2 = __builtin_amdgcn_s_memtime();
-        sr = quad_sum(pr);
-        sz = quad_sum(pz);
-        sn = quad_sum(pn);
-        asm volatile("" :: "v"(sr), "v"(sz), "v"(sn));
-        s3 = __builtin_amdgcn_s_memtime();
-      } else {
+      {
         const f32x4* hv4 = (const f32x4*)(&hb[16 * q]);
         f32x2 ar = {0.0f, 0.0f}, az = {0.0f, 0.0f}, an = {0.0f, 0.0f};
 #pragma unroll
@@ -421,56 +336,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const float h1 = (hprev - ng) * zg + ng;   // ATen gru_cell: (hx - n) * z + n
       hprev = h1;
       if (q == 0) S.hs[c & 1][p][j] = h1;
-      if (online && !(VAR & 1)) {
+      if (online) {
         buf_st(buf_rsrc(Hz + (int64_t)t * RH), hlo, h1);   // wave-uniform bases; lanes q != 0 drop the h store
         buf_st(buf_rsrc(w.Gates + (int64_t)t * (4 * RH)), glo, fmaf(m0, rg, fmaf(m1, zg, fmaf(m2, ng, m3 * ghn))));
       }
-      if (VAR & 2048) s4 = __builtin_amdgcn_s_memtime();
       lds_barrier();
-      if (VAR & 2048) {
-        const uint64_t s5 = __builtin_amdgcn_s_memtime();
-        ph[0] += s1 - s0; ph[1] += s2 - s1; ph[2] += s3 - s2; ph[3] += s4 - s3; ph[4] += s5 - s4;
-      }
     };
     // the chains of both nets issue ahead of every producer wave on the CU (the online workgroups are older and
-    // would otherwise win arbitration against the target chain too); VAR 128 turns this off for A/B runs
-    if (VAR & 1024) {
-      if (online) __builtin_amdgcn_s_setprio(2);
-      else __builtin_amdgcn_s_setprio(3);
-    }
-    else if (!(VAR & 128)) __builtin_amdgcn_s_setprio(2);
-    uint64_t c0 = 0, r0t = 0;
-    if (VAR & 2) { c0 = __builtin_amdgcn_s_memtime(); r0t = __builtin_amdgcn_s_memrealtime(); }
-    if (VAR & 8) {   // diagnostic only: shader cycles per step phase p, summed over the chunks
-      uint64_t bins[FCH];
-#pragma unroll
-      for (int i = 0; i < FCH; ++i) bins[i] = 0;
-      for (int t = 0; t < Tp; ++t) {
-        const uint64_t a = __builtin_amdgcn_s_memtime();
-        step(t);
-        const uint64_t e = __builtin_amdgcn_s_memtime();
-#pragma unroll
-        for (int i = 0; i < FCH; ++i)
-          if (i == (t & (FCH - 1))) bins[i] += e - a;
-      }
-      if (tid == 0) {
-#pragma unroll
-        for (int i = 0; i < FCH; ++i)
-          ((uint64_t*)w.slab_mix)[FCH * bid + i] = bins[i];
-      }
-    } else {
-      for (int t = 0; t < Tp; ++t) step(t);
-    }
+    // would otherwise win arbitration against the target chain too)
+    __builtin_amdgcn_s_setprio(2);
+    for (int t = 0; t < Tp; ++t) step(t);
     __builtin_amdgcn_s_setprio(0);
-    if ((VAR & 2048) && tid == 0) {
-#pragma unroll
-      for (int i = 0; i < 5; ++i) ((uint64_t*)w.slab_mix)[16 * bid + 8 + i] = ph[i];
-    }
-    if ((VAR & 2) && tid == 0) {   // diagnostic only: shader cycles and 100 MHz ticks of the whole T loop
-      const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-      ((uint64_t*)w.slab_mix)[2 * bid] = c1 - c0;
-      ((uint64_t*)w.slab_mix)[2 * bid + 1] = r1 - r0t;
-    }
     return;
   }
 
@@ -503,7 +379,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const bool live = gs != -1, ok = live && t0 + i < Tp;   // (i >= 8 sets the sign bit: compare with -1)
       // a slot past the block writes the never-read pad column xin[0][FXP - 1] and drops its global store
       (&S.xin[0][0])[live ? i * FXP + col : FXP - 1] = ok ? xr[s] : 0.0f;
-      if (online && !(VAR & 32)) buf_st(xr_rsrc, ok ? ((uint32_t)i * RI + col) * 4 : kDrop, xr[s]);
+      if (online) buf_st(xr_rsrc, ok ? ((uint32_t)i * RI + col) * 4 : kDrop, xr[s]);
     }
     // actions_onehot[t-1] is zero unless slot t-1 was filled (runner contract)
     if (s1 == NG && ptid < FCH) {
@@ -520,7 +396,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       if (d.last_action && col < A) v = col == S.aprev[i] ? 1.0f : 0.0f;
       else v = (col - (d.last_action ? A : 0)) == ag ? 1.0f : 0.0f;
       S.xin[i][O + col] = v;
-      if (online && !(VAR & 32)) buf_st(xo, t < Tp ? (ro + col) * 4 : kDrop, v);   // rows past Tp drop
+      if (online) buf_st(xo, t < Tp ? (ro + col) * 4 : kDrop, v);   // rows past Tp drop
     }
   };
   f32x4 acc1 = {0, 0, 0, 0}, acc1b = {0, 0, 0, 0}, accg[3] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
@@ -545,7 +421,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       const int i = 4 * g + e, t = t0 + i;
       const float x = fmaxf((acc1[e] + acc1b[e]) + b1, 0.0f);
       S.x1[i][16 * wv + c16] = x;
-      if (online && !(VAR & 32)) buf_st(xb, t < Tp ? (lo + e * RH) * 4 : kDrop, x);
+      if (online) buf_st(xb, t < Tp ? (lo + e * RH) * 4 : kDrop, x);
     }
     acc1 = f32x4{0, 0, 0, 0};
     acc1b = f32x4{0, 0, 0, 0};
@@ -595,87 +471,46 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   };
 
   // chunk 0 synchronously (5 barriers, matched by the recurrence waves)
-  uint64_t* stp = (uint64_t*)w.slab_mix + 16 * bid;
-  auto stamp = [&](int k) {   // VAR bit 64 (microbenchmark): prologue milestones, 100 MHz ticks
-    if ((VAR & 64) && ptid == 0) stp[k] = __builtin_amdgcn_s_memrealtime();
-  };
-  stamp(1);
   drain_vmem();   // chunk 0's gather (issued before the weight loads)
-  stamp(2);
   lds_barrier();   // 1: weights, padding staged
-  stamp(3);
   store_gather(0);
   lds_barrier();   // 2
   onehots(0);
   lds_barrier();   // 3
-  stamp(4);
   fc1_part(0, FKQ / 4);
   fc1_epi(0);
   lds_barrier();   // 4
-  stamp(5);
   gi_part(0, 16);
   gi_epi(0);
-  if ((VAR & 512) && cl >= 1) issue_gather(1);
   lds_barrier();   // 5
-  stamp(6);
 
-  if (!(VAR & 4)) {
-    for (int c = 0; c <= cl; ++c) {
-      const int t0 = FCH * c;
-      const bool next = c + 1 <= cl;
+  for (int c = 0; c <= cl; ++c) {
+    const int t0 = FCH * c;
+    const bool next = c + 1 <= cl;
 #pragma unroll
-      for (int p = 0; p < FCH; ++p) {
-        if (t0 + p >= Tp) continue;   // last chunk: no work past Tp (no work for chunk c+1 either)
-        if (VAR & 512) {
-          // rebalanced: producer work in every phase, gathers two chunks ahead
-          if (p == 0 && c >= 1) fc2_partial(c - 1);
-          if (p == 1 && c >= 1) fc2_store(c - 1);
-          if (next) {
-            if (p == 2) store_gather(c + 1, 0, 3);
-            if (p == 3) store_gather(c + 1, 3, NG);
-            if (p == 4) onehots(c + 1);
-            if (p == 5) { fc1_part(0, 2); if (c + 2 <= cl) issue_gather(c + 2); }
-            if (p == 6) fc1_part(2, 4);
-            if (p == 7) fc1_part(4, 6);
-            if (p == 8) { fc1_part(6, 8); fc1_epi(c + 1); }
-            if (p == 9) gi_part(0, 3);
-            if (p == 10) gi_part(3, 5);
-            if (p == 11) gi_part(5, 7);
-            if (p == 12) gi_part(7, 9);
-            if (p == 13) gi_part(9, 11);
-            if (p == 14) gi_part(11, 13);
-            if (p == 15) { gi_part(13, 16); gi_epi(c + 1); }
-          }
-          lds_barrier();
-          continue;
-        }
-        if (p == 0) {
-          if (c >= 1) fc2_partial(c - 1);
-          if (next && (!(VAR & 256) || c == 0)) issue_gather(c + 1);
-        }
-        // VAR 256: chunk c+2's gather right after chunk c+1's was staged (15 steps of latency instead of 5)
-        if ((VAR & 256) && p == 6 && c + 2 <= cl) issue_gather(c + 2);
-        if (p == 1 && c >= 1) fc2_store(c - 1);
-        if (next) {
-          if (p == 5) store_gather(c + 1);
-          if (p == 6) onehots(c + 1);
-          if (p == 7) fc1_part(0, 2);
-          if (p == 8) fc1_part(2, 4);
-          if (p == 9) fc1_part(4, 6);
-          if (p == 10) { fc1_part(6, 8); fc1_epi(c + 1); }
-          if (p == 11) gi_part(0, 4);
-          if (p == 12) gi_part(4, 7);
-          if (p == 13) gi_part(7, 10);
-          if (p == 14) gi_part(10, 13);
-          if (p == 15) { gi_part(13, 16); gi_epi(c + 1); }
-        }
-        lds_barrier();
+    for (int p = 0; p < FCH; ++p) {
+      if (t0 + p >= Tp) continue;   // last chunk: no work past Tp (no work for chunk c+1 either)
+      if (p == 0) {
+        if (c >= 1) fc2_partial(c - 1);
+        if (next) issue_gather(c + 1);
       }
+      if (p == 1 && c >= 1) fc2_store(c - 1);
+      if (next) {
+        if (p == 5) store_gather(c + 1);
+        if (p == 6) onehots(c + 1);
+        if (p == 7) fc1_part(0, 2);
+        if (p == 8) fc1_part(2, 4);
+        if (p == 9) fc1_part(4, 6);
+        if (p == 10) { fc1_part(6, 8); fc1_epi(c + 1); }
+        if (p == 11) gi_part(0, 4);
+        if (p == 12) gi_part(4, 7);
+        if (p == 13) gi_part(7, 10);
+        if (p == 14) gi_part(10, 13);
+        if (p == 15) { gi_part(13, 16); gi_epi(c + 1); }
+      }
+      lds_barrier();
     }
-  } else {
-    for (int t = 0; t < Tp; ++t) lds_barrier();
   }
-  stamp(7);
   // the last chunk (and the previous one's store when the last chunk is a single step) after the final barrier,
   // in wave 0 alone
   if (cl >= 1 && Tp - FCH * cl < 2) fc2_store(cl - 1);
@@ -697,38 +532,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       if (t < Tp && c16 < A) Qz[((int64_t)t * R + r) * A + c16] = (q0[e] + q1[e]) + b2;
     }
   }
-  stamp(8);
 }
 
 // Host: the fused forward with the smallest gather-slot instantiation that covers O.
-template <int VAR = 0>
-inline void launch_fwd_fused_v(dim3 grid, hipStream_t s, const Dims& d, const Rep& rp, const float* P0,
-                               const float* P1, const Lay& L, const Work& w) {
+inline void launch_fwd_fused(dim3 grid, hipStream_t s, const Dims& d, const Rep& rp, const float* P0, const float* P1,
+                             const Lay& L, const Work& w) {
   if (FCH * d.O <= 256 * 5)
-    hipLaunchKernelGGL((gru_fwd_fused_kernel<VAR, 5>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
+    hipLaunchKernelGGL((gru_fwd_fused_kernel<5>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
   else
-    hipLaunchKernelGGL((gru_fwd_fused_kernel<VAR, FGATHER>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
+    hipLaunchKernelGGL((gru_fwd_fused_kernel<FGATHER>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
 }
 // The production forward with the QMIX hypernet's workgroups appended (HYP = 1; the caller checked hyf_ok).
 inline void launch_fwd_fused_hyp(hipStream_t s, const Dims& d, const Rep& rp, const float* P0, const float* P1,
                                  const Lay& L, const Work& w) {
   const dim3 grid(2 * d.R + 2 * ((d.M + 31) / 32));
   if (FCH * d.O <= 256 * 5)
-    hipLaunchKernelGGL((gru_fwd_fused_kernel<0, 5, 1>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
+    hipLaunchKernelGGL((gru_fwd_fused_kernel<5, 1>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
   else
-    hipLaunchKernelGGL((gru_fwd_fused_kernel<0, FGATHER, 1>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
-}
-// MQ_FWD_VAR (A/B runs of the schedule variants in the real pipeline, where the obs gather reads cold HBM):
-// 128 chains without priority, 256 gathers two chunks ahead, 512 the rebalanced schedule. Unset = production. Only
-// result-preserving variants are reachable here; the diagnostic bits (no loads / no stores) stay in rec_micro.
-inline void launch_fwd_fused(dim3 grid, hipStream_t s, const Dims& d, const Rep& rp, const float* P0, const float* P1,
-                             const Lay& L, const Work& w) {
-  static const int var = [] { const char* e = std::getenv("MQ_FWD_VAR"); return e ? std::atoi(e) : 0; }();
-  if (var == 4096) launch_fwd_fused_v<4096>(grid, s, d, rp, P0, P1, L, w);   // K4 mat-vec layout
-  else if (var == 256) launch_fwd_fused_v<256>(grid, s, d, rp, P0, P1, L, w);
-  else if (var == 512) launch_fwd_fused_v<512>(grid, s, d, rp, P0, P1, L, w);
-  else if (var == 128) launch_fwd_fused_v<128>(grid, s, d, rp, P0, P1, L, w);  // no chain priority
-  else launch_fwd_fused_v<0>(grid, s, d, rp, P0, P1, L, w);
+    hipLaunchKernelGGL((gru_fwd_fused_kernel<FGATHER, 1>), grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
 }
 
 }  // namespace mq

@@ -12,8 +12,7 @@
 // Backward:
 //   Dx1Prob : dP1 = (dGI W_ih) * [X1 > 0]
 //   Dw1Prob : [dW1 | db1] = dP1^T XIN                  split-K over (t, row)
-//   Dw1VProb: the same, xin rebuilt from the replay rows (no XIN copy)
-//   DwhProb : [dW_hyper | db_hyper] = dHYP^T S0        split-K over (t, episode)
+// (dW_hyper has its own kernel: dwh_kernel.hpp)
 #pragma once
 #include "gemm_f32.hpp"
 #include "learner_types.hpp"
@@ -59,7 +58,6 @@ struct Fc1Prob {
   float* X1;   // [2][M][H]
   float* XIN;  // [M][I], written once
   int64_t M;
-  int32_t* rowtab = nullptr;   // [M][2] replay-row table for Dw1VProb (written by the net-0 column block)
   using APat = KPat;
   using BPat = KPat;
   static constexpr bool kRowSum = false;
@@ -82,8 +80,6 @@ struct Fc1Prob {
       c.ag = ag;
       // actions_onehot[t-1] is zero unless slot t-1 was filled (runner contract, synthetic.py)
       if (d.last_action && t > 0 && rp.filled[slot - 1]) c.aprev = (int)rp.actions[(slot - 1) * d.n + ag];
-      if (rowtab && (tid & 3) == 0 && blockIdx.y == 0)
-        *(int2*)(rowtab + 2 * (int64_t)c.m) = int2{(int)(slot * d.n + ag), (c.aprev + 1) | (ag << 16)};
     }
     const int nn = KPat::row(tid);   // < H: pass p covers net p's 64 output units
     c.brow[0] = P0 + o_w + (int64_t)nn * d.I;
@@ -386,162 +382,6 @@ struct Dw1Prob {
   }
   MQ_DEV void rowsum_out(int j, int z, float v) const {
     if (j < H) slab[(int64_t)z * (H * I + H) + H * I + j] = v;
-  }
-};
-
-// The same [dW1 | db1] slab with the agent inputs built on the fly from the replay rows (Fc1Prob's gather and
-// one-hot columns) instead of read back from a dense XIN copy: at configs[2] (RT = 625,536, I = 348) that copy is
-// 871 MB written by fc1 and read again here. The B operand is staged like Dw1Prob's (MPat); each K-row (row tr of the
-// split) reads tr's entry of the replay-row table fc1 wrote (8 B: obs row, a_{t-1}, agent — 5 MB at configs[2]).
-// Same LDS tile, same k order as Dw1Prob: bitwise the same slab. A/B switch (MQ_DW1_REBUILD=1), not the default:
-// at configs[2] it moves
-// 1.7 GB less per step (fc1 1.17 -> 0.93 ms without the XIN store) but this kernel takes 0.74 ms against
-// Dw1Prob's 0.46 (r03 A/B, profiles/r03_ab_dw1.json): 5.08 vs 5.04 ms a step. Its loads are instruction for
-// instruction Dw1Prob's (same staging, SGPR row bases); what differs is the memory side: XIN is one dense 871 MB
-// stream, the obs rows are 31 KB runs (27 agents x 285 floats of one episode) scattered over the 28 GB replay.
-struct Dw1VProb {
-  static constexpr int BN = 128;
-  Dims d;
-  const float* obs;
-  const int32_t* rowtab;   // [RT][2] from the fc1 pass: obs row index, (a_{t-1} + 1) | agent << 16
-  const float* dP1;   // [RT][H]
-  float* slab;        // [nsplit][H*I + H]
-  int64_t K;          // RT
-  int nsplit;
-  using APat = MPat;
-  using BPat = MPat;
-  static constexpr bool kRowSum = true;
-  // Wave w stages K-rows 4w .. 4w + 3 of each half stage, so the four replay rows it needs are wave-uniform: their
-  // table entries are fetched one stage ahead into VGPRs (nxt*), moved to SGPRs (readfirstlane) when the stage is
-  // staged, and each obs element is then a load from an SGPR row base at the lane's feature offset: the same
-  // 256-byte segments per row as Dw1Prob reads from XIN, with no per-lane address arithmetic.
-  struct Ctx {
-    int n0, kb;
-    mutable int2 nxt0[4], nxt1[4];   // half stage 0 / 1, K-rows 4w + i (static indices only)
-  };
-  MQ_DEV int2 entry(int m, int ke) const { return m < ke ? *(const int2*)(rowtab + 2 * (int64_t)m) : int2{0, 0}; }
-  MQ_DEV Ctx make_ctx(int, int n0, int z, int tid) const {
-    Ctx c;
-    c.n0 = n0;
-    int ke;
-    krange(z, c.kb, ke);
-    const int mb = c.kb + 4 * (tid >> 6);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      c.nxt0[i] = entry(mb + i, ke);
-      c.nxt1[i] = entry(mb + GBK + i, ke);
-    }
-    return c;
-  }
-  MQ_DEV void krange(int z, int& kb, int& ke) const { krange_split((int)K, nsplit, z, kb, ke); }
-  MQ_DEV void load_a(const Ctx&, int k0, int ke, float (&r)[4]) const {
-    const int j = MPat::row(threadIdx.x), k = k0 + MPat::kq(threadIdx.x);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = (k + i < ke) ? dP1[(int64_t)(k + i) * H + j] : 0.0f;
-  }
-  MQ_DEV void load_b(const Ctx& c, int pass, int k0, int ke, float (&r)[4]) const {
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int mb = k0 + 4 * wv;                                  // wave-uniform first K-row
-    const int f = c.n0 + 64 * pass + (threadIdx.x & 63);
-    const bool h1 = ((k0 - c.kb) & GBK) != 0;                    // k0 = kb + GSK * stage + GBK * half
-    int row[4], aux[4];
-    if (h1) {   // uniform branch: the arrays are only ever indexed with constants
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        row[i] = __builtin_amdgcn_readfirstlane(c.nxt1[i].x);
-        aux[i] = __builtin_amdgcn_readfirstlane(c.nxt1[i].y);
-        if (pass == NT_LAST) c.nxt1[i] = entry(mb + GSK + i, ke);   // last pass: fetch the next stage's entries
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        row[i] = __builtin_amdgcn_readfirstlane(c.nxt0[i].x);
-        aux[i] = __builtin_amdgcn_readfirstlane(c.nxt0[i].y);
-        if (pass == NT_LAST) c.nxt0[i] = entry(mb + GSK + i, ke);
-      }
-    }
-    const bool plain = c.n0 + 64 * pass + 63 < d.O;             // uniform: every lane's feature is an obs column
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float v = 0.0f;
-      if (mb + i < ke) {
-        const float* orow = obs + (int64_t)row[i] * d.O;
-        if (plain) {
-          v = orow[f];
-        } else if (f < d.O) {
-          v = orow[f];
-        } else if (f < d.I) {
-          int fo = f - d.O;
-          const int aprev = (aux[i] & 0xffff) - 1, ag = aux[i] >> 16;
-          if (d.last_action) {
-            if (fo < d.A) v = fo == aprev ? 1.0f : 0.0f;
-            fo -= d.A;
-          }
-          if (fo >= 0 && fo == ag) v = 1.0f;
-        }
-      }
-      r[i] = v;
-    }
-  }
-  static constexpr int NT_LAST = BN / 64 - 1;
-  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int z, int lane) const {
-    const int f = ncol0 + (lane & 31);
-    if (f >= d.I) return;
-    float* out = slab + (int64_t)z * (H * d.I + H);
-    for_tile(acc, mrow0, ncol0, lane, [&](int j, int ff, float v) {
-      if (j < H) out[(int64_t)j * d.I + ff] = v;
-    });
-  }
-  MQ_DEV void rowsum_out(int j, int z, float v) const {
-    if (j < H) slab[(int64_t)z * (H * d.I + H) + H * d.I + j] = v;
-  }
-};
-
-// [dW_hyper | db_hyper] slab over the contiguous QMixer region hyper_w_1.weight .. V.0.bias.
-struct DwhProb {
-  static constexpr int BN = 192;
-  Dims d;
-  Lay L;
-  const float* dHYP;   // [M][NH]
-  const float* S0;     // [M][S]
-  float* slab;         // [nsplit][len]
-  int64_t len;
-  int nsplit;
-  using APat = MPat;
-  using BPat = MPat;
-  static constexpr bool kRowSum = true;
-  struct Ctx {
-    int s0;
-  };
-  MQ_DEV Ctx make_ctx(int, int n0, int, int tid) const { return Ctx{n0 + MPat::row(tid)}; }
-  MQ_DEV void krange(int z, int& kb, int& ke) const { krange_split(d.M, nsplit, z, kb, ke); }
-  MQ_DEV void load_a(const Ctx&, int k0, int ke, float (&r)[4]) const {
-    const int j = blockIdx.x * GBM + MPat::row(threadIdx.x), k = k0 + MPat::kq(threadIdx.x);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = (j < d.NH && k + i < ke) ? dHYP[(int64_t)(k + i) * d.NH + j] : 0.0f;
-  }
-  MQ_DEV void load_b(const Ctx& c, int pass, int k0, int ke, float (&r)[4]) const {
-    const int s = c.s0 + 64 * pass, k = k0 + MPat::kq(threadIdx.x);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = (s < d.S && k + i < ke) ? S0[(int64_t)(k + i) * d.S + s] : 0.0f;
-  }
-  MQ_DEV void epilogue(const Ctx&, const f32x16& acc, int mrow0, int ncol0, int z, int lane) const {
-    const int s = ncol0 + (lane & 31);
-    if (s >= d.S) return;
-    float* out = slab + (int64_t)z * len;
-    const int64_t base = L.o[MQ_P_HW1_W];
-    for_tile(acc, mrow0, ncol0, lane, [&](int j, int ss, float v) {
-      if (j < d.NH) {
-        HypSeg sg = hyp_seg(L, d.n * d.E, d.E, j);
-        out[sg.w - base + (int64_t)sg.row * d.S + ss] = v;
-      }
-    });
-  }
-  MQ_DEV void rowsum_out(int j, int z, float v) const {
-    if (j < d.NH) {
-      HypSeg sg = hyp_seg(L, d.n * d.E, d.E, j);
-      slab[(int64_t)z * len + sg.b - L.o[MQ_P_HW1_W] + sg.row] = v;
-    }
   }
 };
 

@@ -60,8 +60,6 @@ struct Work {
   float* XIN;        // [RT][I]  dense agent inputs (written by the fc1 pass, read by dW1)
   float* S0;         // [M][S]   gathered state[:, :-1] rows (written by the hypernet pass, read by dW_hyper)
   float* dHo;        // [RT][H]  COMA actor only: dLogits W2 per (t, row), read by gru_bwd_kernel<.., DY = true>
-  int32_t* rowtab;   // [RT][2]  per (t, row): obs row index, (a_{t-1} + 1) | agent << 16 — written by the fc1
-                     //          pass, read by dW1 when it rebuilds the agent inputs (Dw1VProb)
   // dW_hyper tiles appended to the fused BPTT's grid (gru_bwd_fused.hpp, DWH = 1): slab length, m-slices, j-tiles,
   // tile count
   int64_t dwh_len = 0;

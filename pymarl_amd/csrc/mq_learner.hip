@@ -91,17 +91,12 @@ struct mq_handle {
   // rows run as a second wave of workgroups, which still beats gru_bwd<2> + dX1 + dW1 at configs[3]'s shard
   // (R = 320); MQ_FUSED_BWD_RMAX=256 restores the round-2 cut-over for A/B runs
   int fused_bwd_rmax = getenv("MQ_FUSED_BWD_RMAX") ? atoi(getenv("MQ_FUSED_BWD_RMAX")) : 512;
-  bool force_unfused_mix = getenv("MQ_GEMM_HYPER") != nullptr;   // A/B switch: hypernet through gemm_f32
   int dwh_split = getenv("MQ_DWH_SPLIT") ? atoi(getenv("MQ_DWH_SPLIT")) : 8;   // m-slices of the dW_hyper pass
-  bool generic_mix = getenv("MQ_GENERIC_MIX") != nullptr;   // A/B switch: mix_kernel instead of mix_fast_kernel
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
   ncclComm_t comm = nullptr;   // mq_comm_attach / mq_comm_use: the library all-reduces the grad buffer itself
   int comm_world = 0;
   bool comm_owned = false;     // mq_comm_attach created it (freed on detach); mq_comm_use borrows the caller's
-  // A/B switch, off by default: dW_hyper on a side stream beside the fused BPTT (dwh_kernel.hpp). Measured at cfg2
-  // (r01l): the co-resident dwh_side waves slow the BPTT chain 92.7 -> 105.6 us, the step 238 -> 264 us
-  bool dwh_overlap = getenv("MQ_DWH_OVERLAP") && atoi(getenv("MQ_DWH_OVERLAP")) != 0;
-  hipStream_t side = nullptr;
+  hipStream_t side = nullptr;   // COMA: the actor's side stream (coma_host.hpp)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // QMIX hypernet workgroups appended to the fused forward's grid (gru_fwd_fused.hpp hyper_fwd_body) when the
   // forward's 2R row-nets exceed two per CU: its second wave leaves CUs idle, and the hypernet fills them
@@ -113,22 +108,6 @@ struct mq_handle {
   // (a second wave of rows leaves CUs idle); MQ_DWH_IN_BWD=0 never, =1 always (A/B switches; bitwise either way)
   int dwh_in_bwd = getenv("MQ_DWH_IN_BWD") ? atoi(getenv("MQ_DWH_IN_BWD")) : -1;
   int num_cu = 0;
-  // A/B switch, off by default: mq_train_step runs reduction pass 2 and the optimiser step as one launch
-  // (red_pass2_apply_kernel) unless data parallel. Measured at cfg2 (profiles/r03d_ab_fused_apply): bitwise equal,
-  // 13.2-13.5 us against 12.9-13.1 us for the two launches: the ticket hand-off costs what the launch it removes did
-  bool fuse_apply = getenv("MQ_FUSED_APPLY") && atoi(getenv("MQ_FUSED_APPLY")) == 1;
-  unsigned* ticket = nullptr;   // the fused launch's arrival counter (never reset: tickets continue from ticket_base)
-  unsigned ticket_base = 0;
-  int apply_cap = -1;           // co-resident blocks of red_pass2_apply_kernel (-1: not queried yet)
-  // A/B switch: dW_hyper launched between the mixer and the BPTT instead of after the BPTT (same stream)
-  bool dwh_first = getenv("MQ_DWH_FIRST") && atoi(getenv("MQ_DWH_FIRST")) != 0;
-  // A/B switch: dW_hyper as its own launch before the reduction (default: fused with reduction pass 1)
-  bool dwh_unfused = getenv("MQ_DWH_UNFUSED") && atoi(getenv("MQ_DWH_UNFUSED")) != 0;
-  // A/B switch: the unfused dW1 rebuilds the agent inputs from the replay rows (Dw1VProb) instead of reading fc1's
-  // dense XIN copy, which fc1 then does not write (learner_gemms.hpp: less traffic, slower at configs[2])
-  bool dw1_xin = !(getenv("MQ_DW1_REBUILD") && atoi(getenv("MQ_DW1_REBUILD")) != 0);
-  // register buffers of dW_hyper's m loop (dwh_kernel.hpp): 4 (default) or 2 (A/B switch MQ_DWH_NB=2)
-  int dwh_nb = getenv("MQ_DWH_NB") && atoi(getenv("MQ_DWH_NB")) == 2 ? 2 : 4;
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
   int slots = 0;
   uint32_t mask = 0;
@@ -281,8 +260,7 @@ struct RedBuilder {
     R.tmp = tmp;
     tmp += R.ng * len;
     R.vec = (len % 4 == 0 && R.pitch % 4 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)R.tmp & 15) == 0) ? 1 : 0;
-    static const bool xcd_on = !getenv("MQ_RED_XCD") || atoi(getenv("MQ_RED_XCD")) != 0;   // A/B switch
-    R.xcd = (xcd_on && nslab % 128 == 0 && R.ng == kRedZ && b1 % 16 == 0) ? 1 : 0;
+    R.xcd = (nslab % 128 == 0 && R.ng == kRedZ && b1 % 16 == 0) ? 1 : 0;
     const int nb = (int)((len + 255) / 256), nb1 = R.vec ? (int)((len + 1023) / 1024) : nb;
     R.blk1 = b1; b1 += nb1 * R.ng;
     R.blk2 = b2; b2 += nb;
@@ -290,8 +268,8 @@ struct RedBuilder {
   }
 };
 
-// Side stream and fork / join events of the dW_hyper overlap, created on first use. Lowest stream priority: the
-// BPTT on the caller's stream keeps the arbiter's preference.
+// Side stream and fork / join events (COMA's actor overlap), created on first use. Lowest stream priority: the
+// work on the caller's stream keeps the arbiter's preference.
 hipError_t ensure_side(mq_handle* h) {
   if (h->side) return hipSuccess;
   int least = 0, greatest = 0;
@@ -309,23 +287,6 @@ int device_cus(mq_handle* h) {
                  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess) ? ncu : -1;
   }
   return h->num_cu;
-}
-
-// dW_hyper: 32 x 32 output tiles x nsplit m-slices, operands straight from global memory (dwh_kernel.hpp)
-hipError_t launch_dwh(mq_handle* h, const Dims& d, const Lay& L, const Work& w, hipStream_t s, bool side) {
-  const int tj = (d.NH + DWH_T - 1) / DWH_T, ts = (d.S + 1 + DWH_T - 1) / DWH_T;
-  const int ns = std::max(1, std::min({h->dwh_split, kNsplitMax, (d.M + 1) / 2}));
-  h->nsplit_mix = ns;
-  if (side)
-    hipLaunchKernelGGL(dwh_side_kernel, dim3(tj * ts * ns), dim3(256), 0, s, d, L, (const float*)w.dHYP,
-                       (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj);
-  else if (h->dwh_nb == 2)
-    hipLaunchKernelGGL((dwh_kernel<0, 2>), dim3(tj * ts * ns), dim3(256), 0, s, d, L, (const float*)w.dHYP,
-                       (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj);
-  else
-    hipLaunchKernelGGL((dwh_kernel<0, 4>), dim3(tj * ts * ns), dim3(256), 0, s, d, L, (const float*)w.dHYP,
-                       (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj);
-  return hipGetLastError();
 }
 
 }  // namespace
@@ -371,7 +332,7 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
                           ng(nmix) * (h->E + 1) + ng(nmix) * 8;
   const int64_t norm_parts = (Hd * h->I + Hd + 255) / 256 + (h->len_rnn + 255) / 256 + (h->len_mix + 255) / 256 +
                              (h->E + 1 + 255) / 256 + 1 + 8;
-  int64_t sizes[21] = {
+  int64_t sizes[20] = {
       2 * RT * Hd,                                   // X1
       2 * RT * 3 * Hd,                               // GI
       2 * RT * Hd,                                   // Hs (both nets)
@@ -392,10 +353,9 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
       red_tmp,                                       // two-pass reduction partials
       RT * h->I,                                     // XIN (dense agent inputs)
       Mm * c.state_dim,                              // S0 (gathered state[:, :-1] rows)
-      RT * 4,                                        // rowtab (int32 x 4 per replay row)
   };
-  int64_t total = 0, offs[21];
-  for (int i = 0; i < 21; ++i) { offs[i] = total; total += align_up(std::max<int64_t>(sizes[i], 1)); }
+  int64_t total = 0, offs[20];
+  for (int i = 0; i < 20; ++i) { offs[i] = total; total += align_up(std::max<int64_t>(sizes[i], 1)); }
   hipError_t e = hipMalloc(&h->ws, total * sizeof(float));
   if (e != hipSuccess) {
     delete h;
@@ -413,7 +373,6 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
   w.red_tmp = base + offs[17];
   w.XIN = base + offs[18];
   w.S0 = base + offs[19];
-  w.rowtab = (int32_t*)(base + offs[20]);
   w.curmax = h->curmax_ws;
   *out = h;
   return MQ_OK;
@@ -425,7 +384,6 @@ int mq_destroy(mq_handle* h) {
   for (auto e : h->ev1) (void)hipEventDestroy(e);
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
-  if (h->ticket) (void)hipFree(h->ticket);
   if (h->side) (void)hipStreamDestroy(h->side);
   if (h->ws) (void)hipFree(h->ws);
   if (h->comm && h->comm_owned) (void)ncclCommDestroy(h->comm);
@@ -447,47 +405,20 @@ int mq_bind(mq_handle* h, float* online, float* target, float* grad, float* sq_a
   return MQ_OK;
 }
 
-namespace {
-
-// Whether red_pass2_apply_kernel's grid of nb blocks is co-resident (its tail blocks wait for the others): the
-// occupancy query less one block per CU (the query can run one high, MI355X_MICROARCH.md hazards), times the CUs.
-bool pass2_apply_resident(mq_handle* h, int nb) {
-  if (h->apply_cap < 0) {
-    int dev = 0, ncu = 0, per = 0;
-    h->apply_cap = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, red_pass2_apply_kernel, 256, 0) == hipSuccess)
-      h->apply_cap = std::max(per - 1, 0) * ncu;
-  }
-  return nb >= 1 && nb <= h->apply_cap;
-}
-
-}  // namespace
-
-static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fuse_req, bool* fused_apply);
+static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s);
 
 int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream) {
-  bool fused = false;
-  return fb_impl(h, batch, (hipStream_t)stream, false, &fused);
+  return fb_impl(h, batch, (hipStream_t)stream);
 }
 
 int mq_train_step(mq_handle* h, const mq_replay* batch, void* stream) {
   if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
-  // the optimiser step needs the whole (all-reduced) gradient: with data parallelism it stays a separate pass
-  const bool fuse = !h->dp && !h->comm && h->fuse_apply;
-  bool fused = false;
-  int rc = fb_impl(h, batch, (hipStream_t)stream, fuse, &fused);
+  const int rc = fb_impl(h, batch, (hipStream_t)stream);
   if (rc) return rc;
-  if (fused) {
-    ++h->tstep;
-    return MQ_OK;
-  }
   return mq_apply(h, stream);
 }
 
-static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fuse_req, bool* fused_apply) {
-  *fused_apply = false;
+static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
   if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
   if (!h->on || !h->tg || !h->grad || !h->sq || !h->stats)
     return set_err(MQ_ERR_STATE, "training needs online, target, grad, sq_avg and stats bound (mq_bind)");
@@ -513,11 +444,9 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
     plan.fused_fwd = 1;
     // one row per workgroup: fc1 / W_ih / fc2 ride on the recurrence's idle matrix cores (gru_fwd_fused.hpp)
     pt.begin(PH_GRUF);
-    static const bool fwd_var = getenv("MQ_FWD_VAR") != nullptr;
     const bool two_waves = device_cus(h) > 0 && d.R > h->num_cu;   // 2R row-nets at two per CU
-    hyp_in_fwd = (h->hyp_in_fwd == 1 || (h->hyp_in_fwd < 0 && two_waves)) && !fwd_var &&
-                 c.mixer == MQ_MIXER_QMIX && !h->force_unfused_mix && hyper_ws_ok(d.S, d.E, d.NH, d.M) &&
-                 hyf_ok(d.S, d.E, d.NH, d.M);
+    hyp_in_fwd = (h->hyp_in_fwd == 1 || (h->hyp_in_fwd < 0 && two_waves)) && c.mixer == MQ_MIXER_QMIX &&
+                 hyper_ws_ok(d.S, d.E, d.NH, d.M) && hyf_ok(d.S, d.E, d.NH, d.M);
     if (hyp_in_fwd) {
       plan.hyper = MQ_HYP_WS;
       launch_fwd_fused_hyp(s, d, rp, (const float*)h->on, (const float*)h->tg, L, w);
@@ -529,9 +458,8 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
     plan.rw_fwd = rw_fwd;
     pt.begin(PH_FC1);
     {
-      // the dense agent-input copy is written only for a reader: the fused BPTT, or the XIN form of dW1 (A/B)
-      float* xin = fused_bwd || h->dw1_xin ? w.XIN : nullptr;
-      Fc1Prob p{d, rp, h->on, h->tg, h->off[MQ_P_FC1_W], h->off[MQ_P_FC1_B], w.X1, xin, RT, w.rowtab};
+      // the dense agent-input copy (XIN) is dW1's operand, fused or not
+      Fc1Prob p{d, rp, h->on, h->tg, h->off[MQ_P_FC1_W], h->off[MQ_P_FC1_B], w.X1, w.XIN, RT};
       MQ_HIP(launch_gemm(p, (int)RT, 2 * mq::H, 1, s));
     }
     pt.begin(PH_GI);
@@ -555,14 +483,14 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
   }
   if (c.mixer == MQ_MIXER_QMIX && !hyp_in_fwd) {
     pt.begin(PH_HYP);
-    if (hyper_ws_ok(d.S, d.E, d.NH, d.M) && !h->force_unfused_mix) {
+    if (hyper_ws_ok(d.S, d.E, d.NH, d.M)) {
       plan.hyper = MQ_HYP_WS;
       // wave-specialised weight streaming (hyper_kernel.hpp)
       hipLaunchKernelGGL(hyper_ws_kernel<0>, dim3((d.M + HYR - 1) / HYR, 2), dim3(HYWS_THREADS),
                          hyper_ws_lds_bytes(d.S), s, d, rp, (const float*)h->on, (const float*)h->tg, L, w.HYP,
                          w.S0);
       MQ_HIP(hipGetLastError());
-    } else if (hyper_ok(d.S, d.NH) && !h->force_unfused_mix) {
+    } else if (hyper_ok(d.S, d.NH)) {
       plan.hyper = MQ_HYP_LDS;
       const size_t dyn = HyperGeom(d.S, d.NH).lds_bytes();
       hipLaunchKernelGGL(hyper_kernel<0>, dim3((d.M + HYR - 1) / HYR, 2), dim3(256), dyn, s, d, rp,
@@ -577,7 +505,7 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
   pt.begin(PH_MIX);
   h->nblk_mix = (d.M + 3) / 4;
   {
-    const bool fast = d.n <= 16 && d.E <= 64 && !h->generic_mix;
+    const bool fast = d.n <= 16 && d.E <= 64;   // mix_kernel serves the rest (n > 16 or A > 32)
     plan.mix = fast && d.A <= 16 ? MQ_MIX_FAST16 : fast && d.A <= 32 ? MQ_MIX_FAST32 : MQ_MIX_GENERIC;
     if (fast && d.A <= 16)
       hipLaunchKernelGGL((mix_fast_kernel<16, 16>), dim3(h->nblk_mix), dim3(256), 0, s, d, rp, (const float*)h->on,
@@ -590,28 +518,6 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
                          (const float*)h->tg, L, w, curmax);
     MQ_HIP(hipGetLastError());
   }
-  // dW_hyper needs only the mixer's dHYP: forked onto the side stream it runs in the room the fused BPTT leaves on
-  // each CU, joined before the reduction (same arithmetic in the same order: bitwise the in-order result)
-  const bool side = fused_bwd && c.mixer == MQ_MIXER_QMIX && !h->force_unfused_mix && h->dwh_overlap;
-  if (side) {
-    MQ_HIP(ensure_side(h));
-    MQ_HIP(hipEventRecord(h->ev_fork, s));
-    MQ_HIP(hipStreamWaitEvent(h->side, h->ev_fork, 0));
-    const bool timed = h->slots > 0 && ((h->mask >> PH_DWH) & 1u);
-    const int ti = (int)(h->tstep % std::max(h->slots, 1)) * PH_N + PH_DWH;
-    if (timed) {
-      MQ_HIP(hipEventRecord(h->ev0[ti], h->side));
-      h->ev_used[ti] = 1;
-    }
-    MQ_HIP(launch_dwh(h, d, L, w, h->side, true));
-    if (timed) MQ_HIP(hipEventRecord(h->ev1[ti], h->side));
-    MQ_HIP(hipEventRecord(h->ev_join, h->side));
-  }
-  const bool dwh_first = !side && c.mixer == MQ_MIXER_QMIX && !h->force_unfused_mix && h->dwh_first;
-  if (dwh_first) {
-    pt.begin(PH_DWH);
-    MQ_HIP(launch_dwh(h, d, L, w, s, false));
-  }
   pt.begin(PH_GRUB);
   bool dwh_in_bwd = false;
   plan.fused_bwd = fused_bwd ? 1 : 0;
@@ -621,9 +527,7 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
     h->nblk_bwd = d.R;
     h->nsplit_fc1 = d.R;
     const size_t dyn = ((size_t)2 * d.A * mq::H + d.A) * sizeof(float);
-    static const bool bwd_var = getenv("MQ_BWD_VAR") != nullptr;
-    dwh_in_bwd = c.mixer == MQ_MIXER_QMIX && !h->force_unfused_mix && !h->dwh_overlap && !h->dwh_first &&
-                 !h->dwh_unfused && !bwd_var &&
+    dwh_in_bwd = c.mixer == MQ_MIXER_QMIX &&
                  (h->dwh_in_bwd == 1 || (h->dwh_in_bwd < 0 && device_cus(h) > 0 && d.R > h->num_cu));
     if (dwh_in_bwd) {   // the reduction's dW_hyper blocks, same geometry (see dwh_fused below)
       w.dwh_tj = (d.NH + DWH_T - 1) / DWH_T;
@@ -660,36 +564,12 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
       int64_t chunk = ((RT + ns - 1) / ns + GBK - 1) / GBK * GBK;
       ns = (int)((RT + chunk - 1) / chunk);
       h->nsplit_fc1 = ns;
-      if (h->dw1_xin) {
-        Dw1Prob p{d.I, w.dP1, w.XIN, w.slab_fc1, RT, ns};
-        MQ_HIP(launch_gemm(p, mq::H, d.I, ns, s));
-      } else {   // agent inputs rebuilt from the replay rows (bitwise the XIN form)
-        Dw1VProb p{d, rp.obs, w.rowtab, w.dP1, w.slab_fc1, RT, ns};
-        MQ_HIP(launch_gemm(p, mq::H, d.I, ns, s));
-      }
+      Dw1Prob p{d.I, w.dP1, w.XIN, w.slab_fc1, RT, ns};
+      MQ_HIP(launch_gemm(p, mq::H, d.I, ns, s));
     }
   }
-  // dW_hyper runs fused with pass 1 of the reduction (dwh_red1_kernel) unless an A/B switch placed it elsewhere
-  const bool dwh_fused = c.mixer == MQ_MIXER_QMIX && !side && !dwh_first && !h->force_unfused_mix && !h->dwh_unfused &&
-                         !dwh_in_bwd;
-  if (c.mixer == MQ_MIXER_QMIX && !side && !dwh_first && !dwh_fused && !dwh_in_bwd) {
-    pt.begin(PH_DWH);
-    if (!h->force_unfused_mix) {
-      MQ_HIP(launch_dwh(h, d, L, w, s, false));
-    } else {
-    const int tiles = ((d.NH + GBM - 1) / GBM) * ((d.S + DwhProb::BN - 1) / DwhProb::BN);
-    int ns = std::max(1, std::min(kNsplitMax, std::min((512 + tiles - 1) / tiles, d.M / 64)));
-    int64_t chunk = ((d.M + ns - 1) / ns + GBK - 1) / GBK * GBK;
-    ns = (int)((d.M + chunk - 1) / chunk);
-    h->nsplit_mix = ns;
-    DwhProb p{d, L, w.dHYP, w.S0, w.slab_mix, h->len_mix, ns};
-    MQ_HIP(launch_gemm(p, d.NH, d.S, ns, s));
-    }
-  }
-  if (side) {   // join: the reduction reads dW_hyper's slabs
-    pt.end();
-    MQ_HIP(hipStreamWaitEvent(s, h->ev_join, 0));
-  }
+  // dW_hyper runs fused with pass 1 of the reduction (dwh_red1_kernel), unless its tiles rode in the BPTT's grid
+  const bool dwh_fused = c.mixer == MQ_MIXER_QMIX && !dwh_in_bwd;
   {
     int tj = 0, ts = 0, ns = 0, ndwh = 0;
     if (dwh_fused) {
@@ -714,12 +594,8 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
     if (dwh_fused) {
       pt.begin(PH_DWH);
       const int ndwh_pad = (ndwh + 15) / 16 * 16;
-      if (h->dwh_nb == 2)
-        hipLaunchKernelGGL(dwh_red1_kernel<2>, dim3(ndwh_pad + rb.b1), dim3(256), 0, s, d, L, (const float*)w.dHYP,
-                           (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj, ndwh, ndwh_pad, rb.pl);
-      else
-        hipLaunchKernelGGL(dwh_red1_kernel<4>, dim3(ndwh_pad + rb.b1), dim3(256), 0, s, d, L, (const float*)w.dHYP,
-                           (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj, ndwh, ndwh_pad, rb.pl);
+      hipLaunchKernelGGL(dwh_red1_kernel<4>, dim3(ndwh_pad + rb.b1), dim3(256), 0, s, d, L, (const float*)w.dHYP,
+                         (const float*)w.S0, w.slab_mix, h->len_mix, ns, tj, ndwh, ndwh_pad, rb.pl);
       MQ_HIP(hipGetLastError());
       pt.begin(PH_RED);
     } else {
@@ -729,29 +605,12 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s, bool fus
         MQ_HIP(hipGetLastError());
       }
     }
-    // applying blocks: kApplyTail, or enough that kApplyMaxE elements per thread cover the parameters
-    const int tail = (int)std::max<int64_t>(std::min(kApplyTail, rb.b2), (h->P + 256 * kApplyMaxE - 1) / (256 * kApplyMaxE));
-    if (fuse_req && tail <= rb.b2 && pass2_apply_resident(h, rb.b2)) {
-      if (!h->ticket) {
-        MQ_HIP(hipMalloc(&h->ticket, 256));
-        MQ_HIP(hipMemset(h->ticket, 0, 256));
-        h->ticket_base = 0;
-      }
-      // pass 2 and the optimiser step in one launch (optim_kernels.hpp)
-      const OptHP hp{h->cfg.lr, h->cfg.optim_alpha, h->cfg.optim_eps, h->cfg.grad_norm_clip, h->cfg.n_agents};
-      hipLaunchKernelGGL(red_pass2_apply_kernel, dim3(rb.b2), dim3(256), 0, s, rb.pl, w.norm_part, h->ticket,
-                         h->ticket_base, tail, h->on, h->grad, h->sq, h->P, hp, h->stats);
-      MQ_HIP(hipGetLastError());
-      h->ticket_base += (unsigned)rb.b2;
-      *fused_apply = true;
-    } else {
-      hipLaunchKernelGGL(red_pass2_kernel, dim3(rb.b2), dim3(256), 0, s, rb.pl, w.norm_part);
-      MQ_HIP(hipGetLastError());
-    }
+    hipLaunchKernelGGL(red_pass2_kernel, dim3(rb.b2), dim3(256), 0, s, rb.pl, w.norm_part);
+    MQ_HIP(hipGetLastError());
     h->n_norm_part = rb.b2;
   }
   pt.end();
-  if (h->comm && !*fused_apply) {   // native data parallelism: the whole [grads | sums] buffer, summed over the ranks in stream order
+  if (h->comm) {   // native data parallelism: the whole [grads | sums] buffer, summed over the ranks in stream order
     const ncclResult_t r = ncclAllReduce(h->grad, h->grad, (size_t)(h->P + MQ_NSUMS), ncclFloat, ncclSum, h->comm, s);
     if (r != ncclSuccess) return set_err(MQ_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
   }

@@ -172,130 +172,6 @@ __global__ __launch_bounds__(256) void apply_kernel(float* __restrict__ p, float
   }
 }
 
-// Reduction pass 2 and the optimiser step in ONE launch (mq_train_step without data parallelism). Pass 2 runs as in
-// red_pass2_kernel, but every word it hands over (gradient elements, loss sums, norm partials) is stored
-// write-through (sc1); once all its waves' stores have drained, each block takes a ticket from one agent-scope
-// counter. The last `tail` blocks to arrive wait until the count covers the grid (everyone else has already
-// arrived or is about to: a short wait, not a grid barrier) and then run apply_kernel's update over a 1/tail slice
-// each (at most kApplyMaxE elements per thread, loaded together), reading the handed-over words with sc1 loads (MI355X_MICROARCH.md hand-off table, row 1: one lane per
-// storing workgroup adds to one counter after a workgroup barrier behind every wave's vmcnt(0); the consumer polls
-// the counter with sc1 loads; 4-B sc1 stores and loads). The sums are apply_kernel's, in its order, from the same
-// partials: bitwise the two-launch result. The counter is never reset: launch k's tickets are base_k .. base_k + nb
-// (the handle keeps base_k, unsigned wrap-around arithmetic). The host uses this kernel only when its whole grid is
-// co-resident, so the waiting blocks never hold a slot a late block needs; the spin is bounded anyway, and a timeout
-// skips the update and writes NaN loss / grad_norm stats (loud in the logs, parameters untouched).
-typedef __attribute__((address_space(1))) unsigned opt_gu32;
-MQ_DEV void opt_st_wt(float* p, float v) {
-  __hip_atomic_store((opt_gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-MQ_DEV float opt_ld_wt(const float* p) {
-  return __uint_as_float(__hip_atomic_load((opt_gu32*)(float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-constexpr unsigned kTicketSpin = 1u << 22;
-constexpr int kApplyTail = 128;   // blocks that apply (at least; more when n > kApplyTail * 256 * kApplyMaxE)
-constexpr int kApplyMaxE = 4;     // elements per applying thread
-
-__global__ __launch_bounds__(256) void red_pass2_apply_kernel(RedPlan pl, float* __restrict__ norm_part,
-                                                              unsigned* __restrict__ ticket, unsigned base, int tail,
-                                                              float* __restrict__ p, float* __restrict__ g,
-                                                              float* __restrict__ sq, int64_t n, OptHP hp,
-                                                              float* __restrict__ stats) {
-  __shared__ float red[4];
-  __shared__ unsigned tk;
-  __shared__ float sh[2];
-  {   // ---- pass 2 (red_pass2_kernel's arithmetic, write-through stores)
-    const int k = red_region(pl, blockIdx.x, true);
-    const RedRegion& R = pl.r[k];
-    const int64_t i = (int64_t)(blockIdx.x - R.blk2) * 256 + threadIdx.x;
-    float sv = 0.0f;
-    if (i < R.len) {
-      float u[kRedZ];
-#pragma unroll
-      for (int gg = 0; gg < kRedZ; ++gg) u[gg] = gg < R.ng ? R.tmp[(int64_t)gg * R.tpitch + i] : 0.0f;
-      float v = 0.0f;
-#pragma unroll
-      for (int gg = 0; gg < kRedZ; ++gg) v += u[gg];
-      opt_st_wt(R.dst + i, v);
-      if (R.sq) sv = v * v;
-    }
-    sv = wave_sum(sv);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sv;
-    __syncthreads();
-    if (threadIdx.x == 0) opt_st_wt(norm_part + blockIdx.x, (red[0] + red[1]) + (red[2] + red[3]));
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's write-through stores have left
-  __syncthreads();
-  if (threadIdx.x == 0)
-    tk = __hip_atomic_fetch_add((opt_gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base;
-  __syncthreads();
-  const unsigned nb = gridDim.x, first = nb - (unsigned)tail;
-  if (tk < first) return;
-  const int a = (int)(tk - first);   // this block's apply slice
-  float pvv[kApplyMaxE], svv[kApplyMaxE];
-#pragma unroll
-  for (int e = 0; e < kApplyMaxE; ++e) {
-    const int64_t i = ((int64_t)a + (int64_t)e * tail) * 256 + threadIdx.x;
-    pvv[e] = i < n ? p[i] : 0.0f;
-    svv[e] = i < n ? sq[i] : 0.0f;
-  }
-  if (threadIdx.x == 0) {
-    unsigned spins = 0;
-    bool ok = true;
-    while (__hip_atomic_load((opt_gu32*)ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base < nb) {
-      if (++spins > kTicketSpin) { ok = false; break; }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    sh[1] = ok ? 1.0f : 0.0f;
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the handed-over loads below the poll
-  if (sh[1] == 0.0f) {
-    if (a == 0 && threadIdx.x == 0) { stats[0] = __builtin_nanf(""); stats[1] = __builtin_nanf(""); }
-    return;
-  }
-  // ---- apply_kernel's update of elements a * 256 + tid + e * tail * 256 (e < kApplyMaxE; the host sizes tail so
-  // they cover n): every operand of a thread's elements in flight at once, the parameter and square_avg loads
-  // (written by earlier launches) already before the poll above
-  const float* sums = g + n;
-  const float msum = opt_ld_wt(sums + 1);
-  float gv[kApplyMaxE];
-#pragma unroll
-  for (int e = 0; e < kApplyMaxE; ++e) {
-    const int64_t i = ((int64_t)a + (int64_t)e * tail) * 256 + threadIdx.x;
-    gv[e] = i < n ? opt_ld_wt(g + i) : 0.0f;
-  }
-  if (threadIdx.x < 64) {
-    float s = 0.0f;
-    for (int i = threadIdx.x; i < (int)nb; i += 64) s += opt_ld_wt(norm_part + i);
-    s = wave_sum(s);
-    if (threadIdx.x == 0) sh[0] = s;
-  }
-  __syncthreads();
-  const float inv = 1.0f / msum;
-  const float norm = sqrtf(sh[0]) * inv;
-  const float coef = fminf(hp.clip / (norm + 1e-6f), 1.0f);
-#pragma unroll
-  for (int e = 0; e < kApplyMaxE; ++e) {
-    const int64_t i = ((int64_t)a + (int64_t)e * tail) * 256 + threadIdx.x;
-    if (i >= n) break;
-    const float gi = (gv[e] * inv) * coef;
-    g[i] = gi;
-    const float v = svv[e] * hp.alpha + (1.0f - hp.alpha) * (gi * gi);
-    sq[i] = v;
-    p[i] = pvv[e] + (-hp.lr) * (gi / (sqrtf(v) + hp.eps));
-  }
-  if (a == 0 && threadIdx.x == 0) {
-    stats[0] = opt_ld_wt(sums + 0) / msum;
-    stats[1] = norm;
-    stats[2] = opt_ld_wt(sums + 2) / msum;
-    stats[3] = opt_ld_wt(sums + 3) / (msum * (float)hp.n_agents);
-    stats[4] = opt_ld_wt(sums + 4) / (msum * (float)hp.n_agents);
-    stats[5] = msum;
-    stats[6] = coef;
-    stats[7] = 0.0f;
-  }
-}
-
 // One BasicMAC.forward step for every (episode, agent) row: inputs [obs_t | onehot(a_{t-1}) | onehot(agent)],
 // fc1 -> relu -> GRUCell -> fc2. One 256-thread workgroup per row (rollout batches are small).
 // xin_dense != NULL: the inputs are given ([rows][I], RNNAgent.forward); otherwise they are built from the replay.

@@ -17,9 +17,12 @@ every rank passes the SAME global sample to train() and trains its share of it, 
 * "exchange": every rank trains its shard, and the library sums the global per-step mask sums, each live critic
   step's gradient, the critic stat sums and the agent gradient across ranks (T + 3 all-reduces per train;
   include/mc_coma.h, mc_set_data_parallel).
-Under an RCCL process group the exchanges run on the library's own communicator (mc_comm_attach, the id broadcast
-over torch.distributed once), in stream order with no Python callback; other backends call back into
-`dist.all_reduce`.
+The ranks' agreement on the global sample is checked once (`args.learner_dp_check`, dp.check_same_batch): in
+"replicated" mode every rank's critic must see the same batch or the critics drift apart silently. A batch that is
+already a shard is rejected. Under an RCCL process group the exchanges run on the process's library communicator
+(dp.SharedComm: mq_comm_create once, mc_comm_use per handle), in stream order with no Python callback; other backends
+call back into `dist.all_reduce`. A critic-chain timeout on any rank is all-reduced with the agent gradient, so every
+rank rolls the train() back and raises together.
 
 Reference quirk kept on purpose: the actor reads `mac.action_selector.epsilon`, the value the last rollout call of
 select_actions left there (basic_controller.py:64-67).
@@ -35,7 +38,7 @@ from torch.optim import RMSprop
 from .. import _lib
 from ..modules.critics.coma import COMACritic
 from ..modules.flat import pack, rebind
-from .dp import broadcast_comm_id, dp_world, native_comm_wanted, shard_batch, shard_bounds
+from .dp import SharedComm, dp_world, local_shard, native_comm_wanted, shard_bounds
 from .q_learner import replay_view
 from ..components.episode_buffer import is_replay_view
 
@@ -94,6 +97,8 @@ class COMALearner:
         self._handle_key = None
         self._steps = 0
         self.dp = bool(getattr(args, "learner_dp", False))
+        self.dp_check = getattr(args, "learner_dp_check", "first")   # "first" | "always" | "off" (see QLearner)
+        self._dp_checked = None
         self._dp_cb = None
         self._dp_scratch = None
 
@@ -143,7 +148,7 @@ class COMALearner:
             if self._dp_active():
                 rank, world = dp_world()
                 if native_comm_wanted(self._critic.device):
-                    _lib.check(h.lib.mc_comm_attach(h.h, broadcast_comm_id(h.lib, self._critic.device), rank, world))
+                    _lib.check(h.lib.mc_comm_use(h.h, SharedComm.get(h.lib, self._critic.device)))
                     h.native = True
                 else:
                     self._dp_scratch = th.zeros(8 * T, dtype=th.float32, device=self._critic.device)
@@ -192,18 +197,22 @@ class COMALearner:
     # -- reference API ---------------------------------------------------------------------------------------
     def train(self, batch, t_env: int, episode_num: int):
         _lib.require_gpu(self._agent)
-        h = self._get_handle(batch)
         mode = self.dp_mode(batch.batch_size)
         if mode is not None:
             rank, world = dp_world()
-            if mode == "replicated":   # the critic on the whole batch, the actor on this rank's episodes
-                lo, hi = shard_bounds(batch.batch_size, rank, world)
-                if hi <= lo:
-                    raise ValueError("replicated COMA critic: {} episodes for {} ranks".format(batch.batch_size, world))
-                _lib.check(h.lib.mc_set_actor_shard(h.h, lo, hi))
-            else:                      # exchange: this rank's shard through every step, summed in the library
-                _lib.check(h.lib.mc_set_actor_shard(h.h, 0, 0))
-                batch = shard_batch(batch, rank, world)
+            key = (batch.batch_size, getattr(batch, "t_len", batch.max_seq_length), world)
+            check = self.dp_check == "always" or (self.dp_check != "off" and self._dp_checked != key)
+            local = local_shard(batch, rank, world, check=check, device=self._critic.device)   # validates too
+            if check:
+                self._dp_checked = key
+            if mode == "exchange":     # this rank's shard through every step, summed in the library
+                batch = local
+        h = self._get_handle(batch)
+        if mode == "replicated":       # the critic on the whole global batch, the actor on this rank's episodes
+            lo, hi = shard_bounds(batch.batch_size, rank, world)
+            _lib.check(h.lib.mc_set_actor_shard(h.h, lo, hi))
+        elif mode == "exchange":
+            _lib.check(h.lib.mc_set_actor_shard(h.h, 0, 0))
         rep, keep = replay_view(batch)
         eps = float(self.mac.action_selector.epsilon)
         _lib.check(h.lib.mc_train_step(h.h, ctypes.byref(rep), ctypes.c_float(eps), _lib.stream_ptr()))
@@ -212,7 +221,9 @@ class COMALearner:
         steps = int(round(st[9]))
         if steps < 0:
             # the library put the critic back to its pre-train version and skipped the actor update: the learner's
-            # state is this call's starting state (no step counted), so a retry or MQ_COMA_CHAIN=0 can follow
+            # state is this call's starting state (no step counted), so a retry or MQ_COMA_CHAIN=0 can follow. Under
+            # data parallelism the failure word travels with the agent gradient's all-reduce, so every rank rolled
+            # back and raises here together and a retry keeps the ranks' collective sequence in step
             raise _lib.MQError("COMA critic chain: a workgroup hand-off timed out; this train() was rolled back "
                                "(critic and agent unchanged; MQ_COMA_CHAIN=0 selects the three-launch critic)")
         self.critic_training_steps += steps
@@ -304,5 +315,5 @@ class COMALearner:
         return {"prologue": ms[0], "critic_chain": ms[1], "actor": ms[2]}
 
     def critic_path(self):
-        """"chain" (one persistent cooperative launch for the T critic steps), "three_launch", or None before train()."""
+        """"chain" (one persistent launch for the T critic steps), "three_launch", or None before train()."""
         return {1: "chain", 0: "three_launch"}.get(int(self._handle.lib.mc_last_critic_path(self._handle.h)))

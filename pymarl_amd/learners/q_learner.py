@@ -7,11 +7,13 @@ launch sequence of hand-written HIP kernels in libmq_learner.so (include/mq_lear
 device buffers. There is no CPU path: a learner that is not on a HIP device raises.
 
 Data parallel: with `args.learner_dp = True` and torch.distributed initialised (RCCL, one process
-per GPU), each rank trains its shard of the sampled episodes, the unnormalised gradient buffer (+ the loss/mask
-sums in its tail) is summed with ONE all_reduce, and every rank then applies the identical normalised update.
-Under an RCCL process group the learner attaches the library's own communicator (mq_comm_attach, the id broadcast
-over torch.distributed once): the all-reduce is then issued inside mq_forward_backward, in stream order, and a
-train step makes no Python call between its kernels. Other backends (gloo) all-reduce from Python (dp.py).
+per GPU), every rank calls train() with the SAME GLOBAL sample, as run.py:207-219 does unchanged (ranks share the
+seed, so the sampled ids agree; checked once, `args.learner_dp_check`); the learner trains its own contiguous shard
+of the episodes (dp.local_shard), the unnormalised gradient buffer (+ the loss/mask sums in its tail) is summed with
+ONE all_reduce, and every rank then applies the identical normalised update. Under an RCCL process group the learner
+borrows the process's library communicator (dp.SharedComm: mq_comm_create once, mq_comm_use per handle): the
+all-reduce is then issued inside mq_forward_backward, in stream order, and a train step makes no Python call between
+its kernels. Other backends (gloo) all-reduce from Python (dp.py).
 """
 from __future__ import annotations
 
@@ -27,7 +29,7 @@ from torch.optim import RMSprop
 from .. import _lib
 from ..components.episode_buffer import is_replay_view
 from ..modules.flat import pack, rebind
-from .dp import allreduce_grad_buffer, broadcast_comm_id, dp_world, native_comm_wanted
+from .dp import SharedComm, allreduce_grad_buffer, dp_world, local_shard, native_comm_wanted
 from ..modules.mixers.qmix import QMixer
 from ..modules.mixers.vdn import VDNMixer
 
@@ -149,6 +151,10 @@ class QLearner:
         self.target_mac = copy.deepcopy(mac)
         self.log_stats_t = -self.args.learner_log_interval - 1
         self.dp = bool(getattr(args, "learner_dp", False))
+        # "first" (default): check that the ranks passed the same global sample on the first data-parallel train()
+        # and whenever its shape changes; "always": every train(); "off"
+        self.dp_check = getattr(args, "learner_dp_check", "first")
+        self._dp_checked = None
 
         # flat device buffers: [agent params | mixer params] for online and target nets (MQ_P_* order)
         self._mods = [m for m in (self.mac.agent, self.mixer) if m is not None and len(list(m.parameters()))]
@@ -198,9 +204,21 @@ class QLearner:
         import torch.distributed as dist
         return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
+    def _local_batch(self, batch):
+        """Data parallel: this rank's shard of the global sample (dp.local_shard), the ranks' agreement checked per
+        `self.dp_check`."""
+        rank, world = dp_world()
+        key = (batch.batch_size, getattr(batch, "t_len", batch.max_seq_length), world)
+        check = self.dp_check == "always" or (self.dp_check != "off" and self._dp_checked != key)
+        out = local_shard(batch, rank, world, check=check, device=self._online.device)
+        if check:
+            self._dp_checked = key
+        return out
+
     def _get_handle(self, batch):
         T = batch.source.max_seq_length if is_replay_view(batch) else batch.max_seq_length
-        need_b = max(batch.batch_size, getattr(self.args, "batch_size", 1))
+        world = dp_world()[1] if self._dp_active() else 1
+        need_b = max(batch.batch_size, -(-getattr(self.args, "batch_size", 1) // world))
         key = (need_b, T)
         if self._handle is None or self._handle_key[0] < need_b or self._handle_key[1] < T:
             cfg = make_config(self.args, MIXER_IDS[self.args.mixer], input_dim=self.mac.agent.input_dim,
@@ -213,8 +231,8 @@ class QLearner:
             h.dp_on = False
             h.native = False
             if self._dp_active() and native_comm_wanted(self._online.device):
-                rank, world = dp_world()
-                _lib.check(h.lib.mq_comm_attach(h.h, broadcast_comm_id(h.lib, self._online.device), rank, world))
+                # the process's communicator, created once (a handle rebuilt later needs no collective to attach)
+                _lib.check(h.lib.mq_comm_use(h.h, SharedComm.get(h.lib, self._online.device)))
                 h.native = True
             if h.n_params != self.n_params:
                 raise _lib.MQError("parameter layout mismatch: library {} vs modules {}".format(h.n_params,
@@ -225,10 +243,12 @@ class QLearner:
     # -- reference API ---------------------------------------------------------------------------------------
     def train(self, batch, t_env: int, episode_num: int):
         _lib.require_gpu(self._online)
-        h = self._get_handle(batch)
         # decided per call: torch.distributed may be initialised after the handle was created; mq_apply must then
         # recompute the gradient norm from the all-reduced buffer
         dp = self._dp_active()
+        if dp:
+            batch = self._local_batch(batch)
+        h = self._get_handle(batch)
         want = dp or getattr(self, "force_dp_norm", False)
         if want != h.dp_on:
             _lib.check(h.lib.mq_set_data_parallel(h.h, int(want)))

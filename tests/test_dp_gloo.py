@@ -3,6 +3,7 @@ buffer, one all-reduce (pymarl_amd.learners.dp.allreduce_grad_buffer, the call Q
 then division by the global mask sum == the single-process gradient of the whole batch (q_learner.py:97).
 The per-rank gradients come from the numpy oracle (test infrastructure) on each rank's shard of the golden
 cfg2 / ragged batches, so unequal mask sums per shard are exercised."""
+import json
 import os
 import socket
 
@@ -68,3 +69,85 @@ def test_two_rank_gradient_equals_single_process(tmp_path, name):
     g_dp = buf[:P] / msum
     assert np.abs(g_dp - g_full).max() <= 1e-5 * np.abs(g_full).max()
     assert buf[P] / msum == pytest.approx(fw["loss"], rel=1e-5)
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# The data-parallel train() contract (learners/dp.py): every rank passes the SAME GLOBAL sample, exactly as run.py:207-219
+# does; the learner shards it itself, checks once that the ranks agree, and rejects an already-sharded batch. The
+# plumbing runs on CPU here (QLearner built on the host; train() itself needs the GPU).
+
+def _contract_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = {}
+    try:
+        from pymarl_amd import _lib
+        from pymarl_amd.components.episode_buffer import SampledBatch
+        from pymarl_amd.learners.dp import local_shard, shard_bounds
+        from tests.golden_utils import Case
+        from tests.gpu_helpers import build
+        case = Case("cfg2_qmix_ragged")
+        args, buf, mac, learner, logger = build(case, device="cpu", learner_dp=True)
+        ids = case.z["ids"][0]
+        gb = SampledBatch(buf, ids)
+        gb = gb[:, :gb.max_t_filled()]
+        # the learner's own sharding of the global sample (QLearner.train's first step)
+        loc = learner._local_batch(gb)
+        lo, hi = shard_bounds(len(ids), rank, world)
+        res["ids_ok"] = bool(np.array_equal(loc.ep_ids_np, ids[lo:hi]) and loc.t_len == gb.t_len)
+        res["checked"] = learner._dp_checked is not None
+        # an already-sharded batch (the old caller-shards contract) is rejected, never sharded twice
+        try:
+            learner._local_batch(gb.shard(rank, world))
+            res["reshard"] = "accepted"
+        except ValueError:
+            res["reshard"] = "rejected"
+        try:   # time-truncated shard keeps its tag
+            learner._local_batch(gb.shard(rank, world)[:, :gb.t_len - 1])
+            res["reshard_t"] = "accepted"
+        except ValueError:
+            res["reshard_t"] = "rejected"
+        # a dense batch (the buffer_cpu_only flow's .to()) shards the same episodes
+        dense = SampledBatch(buf, ids)[:, :gb.t_len]
+        dense.dense = True
+        dense.data = dense.materialize().data
+        dl = local_shard(dense, rank, world, check=True)
+        res["dense_ok"] = bool(dl.batch_size == hi - lo and th.equal(dl["obs"], dense["obs"][lo:hi]))
+        # ranks that pass different samples: every rank raises (the check is collective)
+        bad = SampledBatch(buf, ids if rank == 0 else ids[::-1].copy())
+        try:
+            local_shard(bad, rank, world, check=True)
+            res["mismatch"] = "accepted"
+        except _lib.MQError:
+            res["mismatch"] = "raised"
+        # "first": the check is not repeated for the same shape; "always" repeats it
+        learner.dp_check = "always"
+        try:
+            learner._local_batch(SampledBatch(buf, ids if rank == 0 else ids[::-1].copy())[:, :gb.t_len])
+            res["always"] = "accepted"
+        except _lib.MQError:
+            res["always"] = "raised"
+        try:   # fewer episodes than ranks
+            local_shard(SampledBatch(buf, ids[:1]), rank, world, check=False)
+            res["tiny"] = "accepted"
+        except ValueError:
+            res["tiny"] = "rejected"
+        # train() still has no CPU path
+        try:
+            learner.train(gb, 0, 0)
+            res["cpu_train"] = "ran"
+        except _lib.MQError:
+            res["cpu_train"] = "raised"
+    finally:
+        dist.destroy_process_group()
+    np.save(out_path.format(rank), np.array([json.dumps(res)]))
+
+
+def test_dp_train_contract_global_sample(tmp_path):
+    out = str(tmp_path / "res{}.npy")
+    mp.spawn(_contract_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        res = json.loads(str(np.load(out.format(r))[0]))
+        assert res == {"ids_ok": True, "checked": True, "reshard": "rejected", "reshard_t": "rejected",
+                       "dense_ok": True, "mismatch": "raised", "always": "raised", "tiny": "rejected",
+                       "cpu_train": "raised"}, (r, res)

@@ -1,7 +1,8 @@
-"""Data-parallel QLearner end to end on the GPU: two ranks share cuda:0, each trains its shard of
-the same global sample through the product path (QLearner.train -> libmq_learner.so with mq_set_data_parallel,
-all-reduce of the fused [grads | sums] buffer between mq_forward_backward and mq_apply), and the result must equal
-one process training the whole batch (q_learner.py:97's global normalisation).
+"""Data-parallel QLearner end to end on the GPU: two ranks share cuda:0 and each passes the SAME
+GLOBAL sample to train(), exactly as the reference's run loop does (run.py:207-219); the learner trains its own shard
+through the product path (QLearner.train -> libmq_learner.so with mq_set_data_parallel, all-reduce of the fused
+[grads | sums] buffer between mq_forward_backward and mq_apply), and the result must equal one process training the
+whole batch (q_learner.py:97's global normalisation).
 
 The collective here is gloo on device tensors (two ranks cannot share one GPU under RCCL); the bench's N>1 path
 makes the same call over RCCL. Ragged episodes give the two shards unequal mask sums.
@@ -34,8 +35,7 @@ def _train(learner, buf, case, rank, world, record):
     for k in range(STEPS):
         gb = SampledBatch(buf, case.z["ids"][k])
         gb = gb[:, :gb.max_t_filled()]
-        batch = gb.shard(rank, world) if world > 1 else gb
-        learner.train(batch, 1000 * k, case.episodes[k])
+        learner.train(gb, 1000 * k, case.episodes[k])   # the global sample on every rank: the learner shards it
         st = learner.last_stats()
         record["stats"].append([st[s] for s in STATS])
         record["grads"].append(flat_grads(learner))
@@ -54,6 +54,22 @@ def _worker(rank, world, port, out_path):
         rec = {"stats": [], "grads": [], "params": []}
         _train(learner, buf, case, rank, world, rec)
         th.cuda.synchronize()
+        from pymarl_amd import _lib
+        from pymarl_amd.components.episode_buffer import SampledBatch
+        p_before = learner._online.detach().cpu().numpy().copy()
+        gb = SampledBatch(buf, case.z["ids"][0])
+        try:   # a pre-sharded batch (the old caller-shards contract) is rejected, not sharded twice
+            learner.train(gb.shard(rank, world), 0, 0)
+            rec["reshard"] = 0
+        except ValueError:
+            rec["reshard"] = 1
+        learner.dp_check = "always"
+        try:   # ranks that pass different samples raise together (collective check), before any kernel runs
+            learner.train(SampledBatch(buf, case.z["ids"][0] if rank == 0 else case.z["ids"][1]), 0, 0)
+            rec["mismatch"] = 0
+        except _lib.MQError:
+            rec["mismatch"] = 1
+        rec["untouched"] = int(np.array_equal(p_before, learner._online.detach().cpu().numpy()))
         if rank == 0:
             np.savez(out_path, **{k: np.asarray(v) for k, v in rec.items()})
     finally:
@@ -66,6 +82,7 @@ def test_two_rank_dp_equals_single_process(tmp_path):
     out = str(tmp_path / "dp.npz")
     mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     dp = np.load(out)
+    assert int(dp["reshard"]) == 1 and int(dp["mismatch"]) == 1 and int(dp["untouched"]) == 1
 
     case = Case(CASE)
     args, buf, mac, learner, logger = build(case)
@@ -171,3 +188,51 @@ def test_two_rank_coma_dp_equals_single_process(tmp_path, name, steps, mode):
     # allows 5e-2 against the oracle for the same reason (tests/test_gpu_coma.py)
     assert rel(dp["agrad"][0], ref["agrad"][0]) < (5e-3 if long_chain else 1e-4)
     assert np.abs(dp["agent"][-1] - ref["agent"][-1]).max() <= 20 * 5e-4
+
+
+# A critic-chain timeout on ONE rank of a replicated data-parallel COMA (the MQ_COMA_CHAIN_FAULT test hook, set on
+# rank 1 only): the failure word rides in the agent gradient's all-reduce, so BOTH ranks restore the critic, skip the
+# actor update and raise, and both learners are bitwise in their pre-train state (a one-rank rollback let
+# the ranks' parameters diverge).
+
+def _coma_fault_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    th.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pymarl_amd import _lib
+        from pymarl_amd.components.episode_buffer import SampledBatch
+        from tests.golden_utils import ComaCase
+        from tests.gpu_helpers import build_coma
+        case = ComaCase("coma_tiny")
+        args, buf, mac, learner, logger = build_coma(case, learner_dp=True, coma_dp_mode="replicated")
+        gb = SampledBatch(buf, case.z["ids"][0])
+        gb = gb[:, :gb.max_t_filled()]
+        mac.action_selector.epsilon = case.epsilon[0]
+        learner.train(gb, 1000, 0)   # a normal step first (handle, chain, all-reduce all warm)
+        th.cuda.synchronize()
+        before = [t.detach().cpu().numpy().copy() for t in (learner._critic, learner._csq, learner._agent,
+                                                              learner._asq)]
+        if rank == 1:
+            os.environ["MQ_COMA_CHAIN_FAULT"] = "1"
+        raised = 0
+        try:
+            learner.train(gb, 2000, 8)
+        except _lib.MQError:
+            raised = 1
+        os.environ.pop("MQ_COMA_CHAIN_FAULT", None)
+        after = [t.detach().cpu().numpy() for t in (learner._critic, learner._csq, learner._agent, learner._asq)]
+        same = int(all(np.array_equal(a, b) for a, b in zip(before, after)))
+        learner.train(gb, 3000, 16)   # and the ranks stay in step afterwards
+        th.cuda.synchronize()
+        ok_after = int(learner.critic_path() == "chain" and np.isfinite(learner.last_stats()["critic_loss"]))
+        np.save(out_path.format(rank), np.array([raised, same, ok_after]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_coma_replicated_chain_fault_rolls_back_every_rank(tmp_path):
+    out = str(tmp_path / "fault{}.npy")
+    mp.spawn(_coma_fault_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        assert np.load(out.format(r)).tolist() == [1, 1, 1], (r, np.load(out.format(r)))

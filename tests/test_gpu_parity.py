@@ -296,7 +296,7 @@ def set_state_from_oracle(learner, o):
         learner._sq.copy_(th.from_numpy(o.flat("sq")))
 
 
-UNFUSED_ENV = ("MQ_UNFUSED_FWD", "MQ_UNFUSED_BWD", "MQ_GEMM_HYPER")
+UNFUSED_ENV = ("MQ_UNFUSED_FWD", "MQ_UNFUSED_BWD")
 
 
 @pytest.mark.parametrize("name,steps,unfused", [
@@ -423,99 +423,6 @@ def test_data_parallel_norm_path_single_rank(cases):
     assert abs(outs[1][1] - outs[0][1]) <= 1e-5 * abs(outs[0][1])
 
 
-@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_vdn", "tiny_qmix"])
-def test_fast_mix_kernel_bitwise(cases, name, monkeypatch):
-    """mix_fast_kernel (every load issued up front) equals the generic mix_kernel bit for bit."""
-    from tests.gpu_helpers import build, flat_params
-    case = get_case(cases, name)
-    outs = []
-    for generic in (False, True):
-        if generic:
-            monkeypatch.setenv("MQ_GENERIC_MIX", "1")
-        else:
-            monkeypatch.delenv("MQ_GENERIC_MIX", raising=False)
-        args, buf, mac, learner, logger = build(case)
-        np.random.seed(case.sampler_seed)
-        for k in range(2):
-            batch = buf.sample(case.B)
-            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
-        outs.append((flat_params(learner), learner.last_stats(), learner.last_cur_max_actions().cpu().numpy()))
-    assert np.array_equal(outs[0][0], outs[1][0])
-    assert outs[0][1] == outs[1][1]
-    assert np.array_equal(outs[0][2], outs[1][2])
-
-
-@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_qmix_ragged", "tiny_qmix", "cfg3_qmix"])
-def test_dwh_fused_reduction_bitwise(cases, name, monkeypatch):
-    """dW_hyper fused with reduction pass 1 (default) equals dW_hyper as its own launch (MQ_DWH_UNFUSED=1) bitwise."""
-    from tests.gpu_helpers import build, flat_grads, flat_params
-    case = get_case(cases, name)
-    outs = []
-    for unfused in ("1", "0"):
-        monkeypatch.setenv("MQ_DWH_UNFUSED", unfused)
-        args, buf, mac, learner, logger = build(case)
-        np.random.seed(case.sampler_seed)
-        for k in range(2):
-            batch = buf.sample(case.B)
-            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
-        th.cuda.synchronize()
-        outs.append((flat_params(learner), flat_grads(learner), learner.last_stats()))
-    assert np.array_equal(outs[0][0], outs[1][0])
-    assert np.array_equal(outs[0][1], outs[1][1])
-    assert outs[0][2] == outs[1][2]
-
-
-@pytest.mark.parametrize("name,unfused", [("wide_qmix", False), ("cfg3_vdn_b128", False), ("tiny_qmix_bare", True),
-                                          ("cfg2_qmix_ragged", True)])
-def test_dw1_rebuilt_inputs_bitwise(cases, name, unfused, monkeypatch):
-    """The unfused dW1 with the agent inputs rebuilt from the replay rows (Dw1VProb, MQ_DW1_REBUILD=1: fc1 writes no
-    dense XIN copy) equals the default dW1 that reads fc1's XIN copy bitwise: last-action / agent-id columns included
-    (tiny_qmix_bare has neither), ragged episodes, device ep-id vectors (wide_qmix) and inline ids."""
-    from tests.gpu_helpers import build, flat_grads, flat_params
-    case = get_case(cases, name)
-    if unfused:
-        for k in UNFUSED_ENV:
-            monkeypatch.setenv(k, "1")
-    outs = []
-    for rebuild in ("0", "1"):
-        monkeypatch.setenv("MQ_DW1_REBUILD", rebuild)
-        args, buf, mac, learner, logger = build(case)
-        np.random.seed(case.sampler_seed)
-        for k in range(2):
-            batch = buf.sample(case.B)
-            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
-        th.cuda.synchronize()
-        outs.append((flat_params(learner), flat_grads(learner), learner.last_stats()))
-        assert learner.last_plan()["fused_bwd"] == 0
-    assert np.array_equal(outs[0][0], outs[1][0])
-    assert np.array_equal(outs[0][1], outs[1][1])
-    assert outs[0][2] == outs[1][2]
-
-
-@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_vdn", "tiny_qmix_full", "cfg4_qmix"])
-def test_fused_pass2_apply_bitwise(cases, name, monkeypatch):
-    """mq_train_step without data parallelism runs reduction pass 2 and the RMSprop step as one launch
-    (red_pass2_apply_kernel: ticket counter, the last blocks to arrive apply); parameters, clipped gradients,
-    square_avg and the five stats equal the two-launch path (MQ_FUSED_APPLY=0) bitwise over up to three steps."""
-    from tests.gpu_helpers import build, flat_grads, flat_params
-    case = get_case(cases, name)
-    outs = []
-    for fused in ("1", "0"):
-        monkeypatch.setenv("MQ_FUSED_APPLY", fused)
-        args, buf, mac, learner, logger = build(case)
-        np.random.seed(case.sampler_seed)
-        for k in range(min(3, len(case.episodes))):
-            batch = buf.sample(case.B)
-            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
-        th.cuda.synchronize()
-        outs.append((flat_params(learner), flat_grads(learner), learner._sq.cpu().numpy(), learner.last_stats()))
-    assert np.array_equal(outs[0][0], outs[1][0])
-    assert np.array_equal(outs[0][1], outs[1][1])
-    assert np.array_equal(outs[0][2], outs[1][2])
-    assert outs[0][3] == outs[1][3]
-    assert all(np.isfinite(v) for v in outs[0][3].values() if isinstance(v, float))
-
-
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg4_qmix", "cfg1_qmix", "tiny_qmix_full", "cfg2_qmix_ragged"])
 def test_hyper_in_forward_grid_bitwise(cases, name, monkeypatch):
     """The QMIX hypernet as workgroups appended to the fused forward's grid (MQ_HYP_IN_FWD=1; the default for shards
@@ -571,7 +478,6 @@ def test_dwh_split_clamped_when_fused(cases, monkeypatch):
     split-16 run's, and both match the oracle teacher-forced."""
     from tests.gpu_helpers import build, flat_grads, flat_params
     case = get_case(cases, "cfg2_qmix")
-    monkeypatch.delenv("MQ_DWH_UNFUSED", raising=False)
     outs = []
     for split in ("32", "16"):
         monkeypatch.setenv("MQ_DWH_SPLIT", split)
@@ -586,23 +492,3 @@ def test_dwh_split_clamped_when_fused(cases, monkeypatch):
     assert np.array_equal(outs[0][1], outs[1][1])
     monkeypatch.setenv("MQ_DWH_SPLIT", "32")
     run_teacher_forced(case, 2, False, monkeypatch)
-
-
-@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_qmix_ragged", "tiny_qmix"])
-def test_dwh_side_stream_bitwise(cases, name, monkeypatch):
-    """dW_hyper on the side stream beside the fused BPTT (MQ_DWH_OVERLAP=1) equals the in-order launch bit for bit."""
-    from tests.gpu_helpers import build, flat_grads, flat_params
-    case = get_case(cases, name)
-    outs = []
-    for overlap in ("1", "0"):
-        monkeypatch.setenv("MQ_DWH_OVERLAP", overlap)
-        args, buf, mac, learner, logger = build(case)
-        np.random.seed(case.sampler_seed)
-        for k in range(2):
-            batch = buf.sample(case.B)
-            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
-        th.cuda.synchronize()
-        outs.append((flat_params(learner), flat_grads(learner), learner.last_stats()))
-    assert np.array_equal(outs[0][0], outs[1][0])
-    assert np.array_equal(outs[0][1], outs[1][1])
-    assert outs[0][2] == outs[1][2]
