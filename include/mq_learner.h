@@ -154,6 +154,8 @@ typedef struct mq_plan {
   int32_t inline_ids;    /* episode ids in the kernel arguments (1) or read from mq_replay.ep_ids (0) */
   int32_t hyper;         /* MQ_HYP_* */
   int32_t mix;           /* MQ_MIX_* */
+  int32_t tiles;         /* 1: the row-tile MFMA forward / BPTT of large batches (gru_fwd_tile / gru_bwd_tile);
+                            fused_fwd / fused_bwd / rw_* are then 0 */
 } mq_plan;
 int mq_last_plan(const mq_handle* h, mq_plan* out);
 

@@ -222,18 +222,23 @@ namespace mq {
 // the mask / reward / terminated words, all in one round trip; only the chosen-action value waits on the action.
 // The generic kernel fetches them in dependent stages (action -> chosen, argmax blocks -> target value, then the
 // hypernet rows after a barrier). Same arithmetic in the same order: bitwise-identical outputs.
+//
+// mix_fast_row is one wave's (t, b) row m: hon / htg point at its hypernet outputs (HYP rows in global memory for
+// mix_fast_kernel, LDS rows for hymix_kernel), `sc` is the wave's LDS scratch, and the row's loss / V.2 partials
+// land in red_slot[0..4] / v2_slot[0..64] for the caller's fixed-order block sums. Two workgroup barriers inside:
+// every wave of the workgroup must call it the same number of times.
+template <int MN>
+struct MixScratch {
+  float chs[64], tms[64], dps[64];
+  float w1s[MN][65];   // |hyper_w_1| rows of the online mixer, for dLoss/dchosen
+};
+
 template <int MA, int MN>
-__global__ __launch_bounds__(256) void mix_fast_kernel(Dims d, Rep rp, const float* __restrict__ P0,
-                                                       const float* __restrict__ P1, Lay L, Work w,
-                                                       int32_t* curmax_out) {
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int m = blockIdx.x * 4 + wv;
+MQ_DEV void mix_fast_row(const Dims& d, const Rep& rp, const float* __restrict__ P0, const float* __restrict__ P1,
+                         const Lay& L, const Work& w, int32_t* curmax_out, int m, int lane, const float* hon,
+                         const float* htg, MixScratch<MN>& sc, float* red_slot, float* v2_slot) {
   const int n = d.n, A = d.A, E = d.E, R = d.R, NH = d.NH;
   const bool qmix = d.mixer == MQ_MIXER_QMIX;
-  __shared__ float chs[4][64], tms[4][64], dps[4][64];
-  __shared__ float w1s[4][MN][65];   // |hyper_w_1| rows of the online mixer, for dLoss/dchosen
-  __shared__ float red[4][8];
-  __shared__ float v2red[4][65];
   float l2 = 0.0f, msk = 0.0f, abs_ = 0.0f, qs = 0.0f, tg = 0.0f;
   float dv2 = 0.0f, dv2b = 0.0f;
   const bool valid = m < d.M;
@@ -270,8 +275,6 @@ __global__ __launch_bounds__(256) void mix_fast_kernel(Dims d, Rep rp, const flo
   const bool e_lane = qmix && valid && lane < E;
   float won[MN], wtg[MN], xon[3], xtg[3], v2w0 = 0.0f, v2w1 = 0.0f;
   if (e_lane) {
-    const float* hon = w.HYP + (int64_t)m * NH;
-    const float* htg = w.HYP + ((int64_t)d.M + m) * NH;
 #pragma unroll
     for (int ag = 0; ag < MN; ++ag) {
       won[ag] = hon[min(ag, n - 1) * E + lane];
@@ -316,11 +319,11 @@ __global__ __launch_bounds__(256) void mix_fast_kernel(Dims d, Rep rp, const flo
     }
     if (curmax_out) curmax_out[(int64_t)t * R + r] = cur;
   }
-  chs[wv][lane] = chosen;
-  tms[wv][lane] = tmax;
+  sc.chs[lane] = chosen;
+  sc.tms[lane] = tmax;
   if (e_lane) {
 #pragma unroll
-    for (int ag = 0; ag < MN; ++ag) w1s[wv][ag][lane] = fabsf(won[ag]);
+    for (int ag = 0; ag < MN; ++ag) sc.w1s[ag][lane] = fabsf(won[ag]);
   }
   __syncthreads();
   const float gamma = d.gamma;
@@ -334,8 +337,8 @@ __global__ __launch_bounds__(256) void mix_fast_kernel(Dims d, Rep rp, const flo
 #pragma unroll
         for (int ag = 0; ag < MN; ++ag) {
           if (ag < n) {
-            acc = fmaf(chs[wv][ag], fabsf(won[ag]), acc);
-            acc_t = fmaf(tms[wv][ag], fabsf(wtg[ag]), acc_t);
+            acc = fmaf(sc.chs[ag], fabsf(won[ag]), acc);
+            acc_t = fmaf(sc.tms[ag], fabsf(wtg[ag]), acc_t);
           }
         }
         pre = acc + xon[1];
@@ -367,14 +370,14 @@ __global__ __launch_bounds__(256) void mix_fast_kernel(Dims d, Rep rp, const flo
       dv2 = dy * fmaxf(xon[2], 0.0f);                                         // V.2 weight
 #pragma unroll
       for (int ag = 0; ag < MN; ++ag)                                         // hyper_w_1 (through |.|)
-        if (ag < n) dh[ag * E + lane] = (chs[wv][ag] * dpre) * sgnf(won[ag]);
+        if (ag < n) dh[ag * E + lane] = (sc.chs[ag] * dpre) * sgnf(won[ag]);
     }
     dv2b = dy;
-    dps[wv][lane] = dpre;
+    sc.dps[lane] = dpre;
     __syncthreads();
     if (agent_lane) {
       float acc = 0.0f;
-      for (int e = 0; e < E; ++e) acc = fmaf(w1s[wv][lane][e], dps[wv][e], acc);
+      for (int e = 0; e < E; ++e) acc = fmaf(sc.w1s[lane][e], sc.dps[e], acc);
       w.dch[(int64_t)t * R + b * n + lane] = acc;
     }
   } else {
@@ -405,10 +408,26 @@ __global__ __launch_bounds__(256) void mix_fast_kernel(Dims d, Rep rp, const flo
   }
   if (!valid) { l2 = msk = abs_ = qs = tg = 0.0f; dv2 = dv2b = 0.0f; }
   if (lane == 0) {
-    red[wv][0] = l2; red[wv][1] = msk; red[wv][2] = abs_; red[wv][3] = qs; red[wv][4] = tg;
-    v2red[wv][64] = dv2b;
+    red_slot[0] = l2; red_slot[1] = msk; red_slot[2] = abs_; red_slot[3] = qs; red_slot[4] = tg;
+    v2_slot[64] = dv2b;
   }
-  v2red[wv][lane] = dv2;
+  v2_slot[lane] = dv2;
+}
+
+template <int MA, int MN>
+__global__ __launch_bounds__(256) void mix_fast_kernel(Dims d, Rep rp, const float* __restrict__ P0,
+                                                       const float* __restrict__ P1, Lay L, Work w,
+                                                       int32_t* curmax_out) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + wv;
+  const int E = d.E, NH = d.NH;
+  const bool qmix = d.mixer == MQ_MIXER_QMIX;
+  __shared__ MixScratch<MN> sc[4];
+  __shared__ float red[4][8];
+  __shared__ float v2red[4][65];
+  const float* hon = w.HYP + (int64_t)m * NH;
+  const float* htg = w.HYP + ((int64_t)d.M + m) * NH;
+  mix_fast_row<MA, MN>(d, rp, P0, P1, L, w, curmax_out, m, lane, hon, htg, sc[wv], red[wv], v2red[wv]);
   __syncthreads();
   if (threadIdx.x < 8) {
     const int c = threadIdx.x;

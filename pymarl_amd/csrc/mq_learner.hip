@@ -27,6 +27,7 @@
 #include "gru_kernels.hpp"
 #include "gru_fwd_fused.hpp"
 #include "gru_bwd_fused.hpp"
+#include "gru_tiles.hpp"
 #include "mix_kernels.hpp"
 #include "hyper_kernel.hpp"
 #include "dwh_kernel.hpp"
@@ -92,6 +93,9 @@ struct mq_handle {
   // (R = 320); MQ_FUSED_BWD_RMAX=256 restores the round-2 cut-over for A/B runs
   int fused_bwd_rmax = getenv("MQ_FUSED_BWD_RMAX") ? atoi(getenv("MQ_FUSED_BWD_RMAX")) : 512;
   int dwh_split = getenv("MQ_DWH_SPLIT") ? atoi(getenv("MQ_DWH_SPLIT")) : 8;   // m-slices of the dW_hyper pass
+  // the row-tile MFMA forward / BPTT (gru_tiles.hpp) for batches past the one-row fused kernels (R > 512 rows);
+  // MQ_ROW_TILES=1 forces it on any batch it can take (tests), =0 turns it off (A/B: the unfused GEMM path)
+  int row_tiles = getenv("MQ_ROW_TILES") ? atoi(getenv("MQ_ROW_TILES")) : -1;
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
   ncclComm_t comm = nullptr;   // mq_comm_attach / mq_comm_use: the library all-reduces the grad buffer itself
   int comm_world = 0;
@@ -437,10 +441,25 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
   plan.rows = d.R;
   plan.inline_ids = rp.nids > 0 ? 1 : 0;
   const int rw_bwd = std::min(2, pick_rw(d.R, 256));
-  const bool fused_bwd = d.R <= h->fused_bwd_rmax && fused_bwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused_bwd;
+  const int kq1 = tile_kq1(d.O);
+  const bool tiles = tiles_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused && !h->force_unfused_bwd &&
+                     (h->row_tiles == 1 || (h->row_tiles < 0 && d.R > 512));
+  const bool fused_bwd = !tiles && d.R <= h->fused_bwd_rmax && fused_bwd_ok(d.I, d.O, d.A, d.n, RT) &&
+                         !h->force_unfused_bwd;
   const int rw_fwd = pick_rw(d.R, 512);
   bool hyp_in_fwd = false;
-  if (rw_fwd == 1 && fused_fwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused) {
+  plan.tiles = tiles ? 1 : 0;
+  if (tiles) {
+    // row tiles of 32 (two M-tiles) per workgroup, both nets: the recurrence and fc1 / W_ih / fc2 on MFMA
+    pt.begin(PH_GRUF);
+    const dim3 grid((d.R + TR_F - 1) / TR_F, 2);
+    const float *P0 = h->on, *P1 = h->tg;
+    if (kq1 == 8) hipLaunchKernelGGL(gru_fwd_tile_kernel<8>, grid, dim3(256), 0, s, d, rp, P0, P1, L, w);
+    else if (kq1 == 20) hipLaunchKernelGGL(gru_fwd_tile_kernel<20>, grid, dim3(256), 0, s, d, rp, P0, P1, L, w);
+    else if (kq1 == 40) hipLaunchKernelGGL(gru_fwd_tile_kernel<40>, grid, dim3(256), 0, s, d, rp, P0, P1, L, w);
+    else hipLaunchKernelGGL(gru_fwd_tile_kernel<80>, grid, dim3(256), 0, s, d, rp, P0, P1, L, w);
+    MQ_HIP(hipGetLastError());
+  } else if (rw_fwd == 1 && fused_fwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused) {
     plan.fused_fwd = 1;
     // one row per workgroup: fc1 / W_ih / fc2 ride on the recurrence's idle matrix cores (gru_fwd_fused.hpp)
     pt.begin(PH_GRUF);
@@ -521,8 +540,19 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
   pt.begin(PH_GRUB);
   bool dwh_in_bwd = false;
   plan.fused_bwd = fused_bwd ? 1 : 0;
-  plan.rw_bwd = fused_bwd ? 0 : rw_bwd;
-  if (fused_bwd) {
+  plan.rw_bwd = fused_bwd || tiles ? 0 : rw_bwd;
+  if (tiles) {
+    const int nblk = (d.R + TR_B - 1) / TR_B;
+    h->nblk_bwd = nblk;
+    h->nsplit_fc1 = nblk;
+    const int64_t l1 = (int64_t)mq::H * d.I + mq::H;
+    const float* P0 = h->on;
+    if (kq1 == 8) hipLaunchKernelGGL(gru_bwd_tile_kernel<8>, dim3(nblk), dim3(256), 0, s, d, rp, P0, L, w, h->len_rnn, l1);
+    else if (kq1 == 20) hipLaunchKernelGGL(gru_bwd_tile_kernel<20>, dim3(nblk), dim3(256), 0, s, d, rp, P0, L, w, h->len_rnn, l1);
+    else if (kq1 == 40) hipLaunchKernelGGL(gru_bwd_tile_kernel<40>, dim3(nblk), dim3(256), 0, s, d, rp, P0, L, w, h->len_rnn, l1);
+    else hipLaunchKernelGGL(gru_bwd_tile_kernel<80>, dim3(nblk), dim3(256), 0, s, d, rp, P0, L, w, h->len_rnn, l1);
+    MQ_HIP(hipGetLastError());
+  } else if (fused_bwd) {
     // one row per workgroup: dW_hh / dW_ih / dX1 / dW1 on the chain's idle matrix cores (gru_bwd_fused.hpp)
     h->nblk_bwd = d.R;
     h->nsplit_fc1 = d.R;

@@ -218,10 +218,11 @@ def test_cfg2_trajectory(cases, name):
 # and gru_bwd_kernel<2> (R > 512); B > 256 sends the episode ids through the device vector; cfg3_vdn_b128 is BASELINE
 # configs[2] itself (the bench's cfg3 path).
 WIDE_PLANS = {
-    "rw2_qmix": dict(rows=576, fused_fwd=0, rw_fwd=2, fused_bwd=0, rw_bwd=2, inline_ids=1, hyper="ws"),
-    "rw4_vdn": dict(rows=1280, fused_fwd=0, rw_fwd=4, fused_bwd=0, rw_bwd=2, inline_ids=1, mix="fast16"),
-    "wide_qmix": dict(rows=2400, fused_fwd=0, rw_fwd=8, fused_bwd=0, rw_bwd=2, inline_ids=0),
-    "cfg3_vdn_b128": dict(rows=3456, fused_fwd=0, rw_fwd=8, fused_bwd=0, rw_bwd=2, inline_ids=1, mix="generic"),
+    # past the one-row fused kernels (R > 512): the row-tile MFMA forward / BPTT (gru_tiles.hpp)
+    "rw2_qmix": dict(rows=576, tiles=1, fused_fwd=0, fused_bwd=0, inline_ids=1, hyper="ws"),
+    "rw4_vdn": dict(rows=1280, tiles=1, fused_fwd=0, fused_bwd=0, inline_ids=1, mix="fast16"),
+    "wide_qmix": dict(rows=2400, tiles=1, fused_fwd=0, fused_bwd=0, inline_ids=0),
+    "cfg3_vdn_b128": dict(rows=3456, tiles=1, fused_fwd=0, fused_bwd=0, inline_ids=1, mix="generic"),
     "cfg2_iql": dict(rows=256, fused_fwd=1, fused_bwd=1, hyper="none"),
     # configs[3]'s per-GPU shard: R = 320 rows, past the CU count, still on the fused BPTT (a second wave of rows)
     "cfg4_qmix": dict(rows=320, fused_fwd=1, fused_bwd=1, hyper="ws"),
@@ -231,6 +232,35 @@ WIDE_PLANS = {
 @pytest.mark.parametrize("name", sorted(WIDE_PLANS))
 def test_wide_batch_paths_vs_reference(cases, name):
     run_case(get_case(cases, name), check_full=False, plan=WIDE_PLANS[name])
+
+
+# The row-batched GEMM + recurrence path the row tiles replaced (MQ_ROW_TILES=0): gru_fwd_kernel<RW> (RW = 2 / 4 / 8
+# rows per workgroup) and gru_bwd_kernel<2>, still the path for shapes past the tiles' limits, pinned to the same
+# reference goldens.
+RW_PLANS = {
+    "rw2_qmix": dict(rows=576, tiles=0, fused_fwd=0, rw_fwd=2, fused_bwd=0, rw_bwd=2, inline_ids=1, hyper="ws"),
+    "rw4_vdn": dict(rows=1280, tiles=0, fused_fwd=0, rw_fwd=4, fused_bwd=0, rw_bwd=2, inline_ids=1),
+    "wide_qmix": dict(rows=2400, tiles=0, fused_fwd=0, rw_fwd=8, fused_bwd=0, rw_bwd=2, inline_ids=0),
+}
+
+
+@pytest.mark.parametrize("name", sorted(RW_PLANS))
+def test_row_batched_paths_vs_reference(cases, name, monkeypatch):
+    monkeypatch.setenv("MQ_ROW_TILES", "0")
+    run_case(get_case(cases, name), check_full=False, plan=RW_PLANS[name])
+
+
+# The row-tile path forced onto every shape it takes (MQ_ROW_TILES=1), teacher-forced against the oracle: partial
+# tiles (R not a multiple of 16 / 32), ragged episodes, VDN / QMIX / IQL, the obs_last_action / obs_agent_id = False
+# branches, configs[2]'s shape at B = 4 and configs[3]'s shard.
+@pytest.mark.parametrize("name,steps", [
+    ("tiny_qmix", 4), ("tiny_vdn", 4), ("tiny_iql", 3), ("tiny_qmix_bare", 3), ("tiny_qmix_nola", 3),
+    ("tiny_vdn_noid", 3), ("cfg2_qmix", 3), ("cfg2_qmix_ragged", 3), ("cfg3_vdn", 3), ("cfg3_qmix", 2),
+    ("cfg4_qmix", 2), ("cfg1_qmix", 3)])
+def test_row_tiles_teacher_forced(cases, name, steps, monkeypatch):
+    monkeypatch.setenv("MQ_ROW_TILES", "1")
+    learner = run_teacher_forced(get_case(cases, name), steps, False, monkeypatch)
+    assert learner.last_plan()["tiles"] == 1
 
 
 @pytest.mark.parametrize("name", ["tiny_qmix", "tiny_vdn"])
@@ -403,7 +433,10 @@ def run_teacher_forced(case, steps, unfused, monkeypatch, flow="view"):
     if flow == "dense_slice":   # every truncated batch is read in place with t_stride = T + 1 > t_len
         assert strided == truncated, (strided, truncated)
         assert case.name != "cfg1_qmix" or strided == steps
-    write_record("teacher" + ("_unfused" if unfused else "") + ("" if flow == "view" else "_" + flow), name, rec)
+    tag = "_tiles" if os.environ.get("MQ_ROW_TILES") == "1" else ""
+    write_record("teacher" + ("_unfused" if unfused else "") + tag + ("" if flow == "view" else "_" + flow), name,
+                 rec)
+    return learner
 
 
 def test_data_parallel_norm_path_single_rank(cases):
