@@ -143,7 +143,8 @@ int mq_qmix_forward(const float* mixer, int32_t n_agents, int32_t state_dim, int
 
 /* Which kernel variants the last mq_forward_backward launched (test / profiling introspection; no device sync).
  * rw_fwd / rw_bwd: rows per workgroup of the unfused recurrences (0 when the fused kernel ran). */
-enum { MQ_HYP_NONE = 0, MQ_HYP_WS = 1, MQ_HYP_LDS = 2, MQ_HYP_GEMM = 3 };
+/* MQ_HYP_MIX: hypernet and mixer in one launch (hymix_kernel); mix then names the mixer instantiation */
+enum { MQ_HYP_NONE = 0, MQ_HYP_WS = 1, MQ_HYP_LDS = 2, MQ_HYP_GEMM = 3, MQ_HYP_MIX = 4 };
 enum { MQ_MIX_FAST16 = 0, MQ_MIX_FAST32 = 1, MQ_MIX_GENERIC = 2 };
 typedef struct mq_plan {
   int32_t rows;          /* R = batch_size * n_agents */

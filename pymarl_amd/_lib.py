@@ -85,7 +85,7 @@ class MQPlan(ctypes.Structure):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
 
 
-HYP_NAMES = {0: "none", 1: "ws", 2: "lds", 3: "gemm"}
+HYP_NAMES = {0: "none", 1: "ws", 2: "lds", 3: "gemm", 4: "ws_mix"}
 MIX_NAMES = {0: "fast16", 1: "fast32", 2: "generic"}
 
 INLINE_IDS = 256   # MQ_INLINE_IDS: batches up to this size pass their episode ids in the kernel arguments

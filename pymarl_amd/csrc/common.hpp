@@ -58,6 +58,10 @@ MQ_DEV __amdgpu_buffer_rsrc_t buf_rsrc(const float* base) {
 MQ_DEV void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, byte_off, 0, 0);
 }
+MQ_DEV void buf_st4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, f32x4 v) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, byte_off, 0, 0);
+}
 
 // Lane exchange inside an aligned group of 4 lanes (DPP quad_perm, no LDS round trip).
 MQ_DEV float quad_xor1(float v) {

@@ -340,7 +340,7 @@ __global__ __launch_bounds__(512) void hymix_kernel(Dims d, Rep rp, const float*
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int z = wv >> 2, wl = wv & 3;
   const int m0 = blockIdx.x * HMX_R;
-  const int Sd = d.S, NH = d.NH, n = d.n, E = d.E, NT = d.NH / 16;
+  const int Sd = d.S, n = d.n, E = d.E, NT = d.NH / 16;
   const float* __restrict__ P = z ? P1 : P0;
   {
     // ---- A operand: state row m0 + c16 at t + z, this lane group's K quarter [48 g, 48 g + 48), zero past S / M
@@ -364,28 +364,37 @@ __global__ __launch_bounds__(512) void hymix_kernel(Dims d, Rep rp, const float*
     // descriptor (past the buffer: 0; past S within a row: the next row's finite values, times the zero A padding)
     const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)P, (short)0, (int)(L.o[MQ_P_COUNT] * sizeof(float)), 0x00020000);
-    float bw[2][48];
-    float bias[2];
-    auto fetch = [&](int nt, float (&dst)[48], float& bj) {
+    // two register sets with compile-time names (the tile loop is unrolled by two): the next tile's 48 loads are
+    // in flight under the current tile's MFMAs
+    // each lane's 48 K values of its weight row are contiguous: 12 dwordx4 loads per lane per tile
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    f32x4 bwa[12], bwb[12];
+    float bja = 0.0f, bjb = 0.0f;
+    auto fetch = [&](int nt, f32x4 (&dst)[12], float& bj) {
       const HypSeg sg = hyp_seg(L, n * E, E, 16 * nt);
       const int base = (int)((sg.w + (int64_t)(sg.row + c16) * Sd + 48 * g) * 4);
 #pragma unroll
-      for (int q = 0; q < 48; ++q)
-        dst[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(prs, 0, base + 4 * q, 0));
+      for (int q = 0; q < 12; ++q)
+        dst[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, base + 16 * q, 0, 0));
       bj = P[sg.b + sg.row + c16];
     };
-    int nt = wl;
-    if (nt < NT) fetch(nt, bw[0], bias[0]);
-    for (int i = 0; nt < NT; ++i, nt += 4) {
-      const int cur = i & 1;
-      if (nt + 4 < NT) fetch(nt + 4, bw[cur ^ 1], bias[cur ^ 1]);
+    auto tile = [&](int nt, const f32x4 (&bw)[12], float bj) {
       f32x4 acc = {0, 0, 0, 0};
 #pragma unroll
       for (int mm = 0; mm < 12; ++mm)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc = mfma16x4(av[mm][e], bw[cur][4 * mm + e], acc);
+        for (int e = 0; e < 4; ++e) acc = mfma16x4(av[mm][e], bw[mm][e], acc);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) S.hyp[z][4 * g + e][16 * nt + c16] = acc[e] + bias[cur];
+      for (int e = 0; e < 4; ++e) S.hyp[z][4 * g + e][16 * nt + c16] = acc[e] + bj;
+    };
+    int nt = wl;
+    if (nt < NT) fetch(nt, bwa, bja);
+    for (; nt < NT; nt += 8) {
+      if (nt + 4 < NT) fetch(nt + 4, bwb, bjb);
+      tile(nt, bwa, bja);
+      if (nt + 4 >= NT) break;
+      if (nt + 8 < NT) fetch(nt + 8, bwa, bja);
+      tile(nt + 4, bwb, bjb);
     }
   }
   __syncthreads();

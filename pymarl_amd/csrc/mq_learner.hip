@@ -96,6 +96,8 @@ struct mq_handle {
   // the row-tile MFMA forward / BPTT (gru_tiles.hpp) for batches past the one-row fused kernels (R > 512 rows);
   // MQ_ROW_TILES=1 forces it on any batch it can take (tests), =0 turns it off (A/B: the unfused GEMM path)
   int row_tiles = getenv("MQ_ROW_TILES") ? atoi(getenv("MQ_ROW_TILES")) : -1;
+  // MQ_HYMIX=1: the QMIX hypernet and mixer in one launch (hymix_kernel, bitwise the two-kernel path)
+  bool hymix = getenv("MQ_HYMIX") && atoi(getenv("MQ_HYMIX")) == 1;
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
   ncclComm_t comm = nullptr;   // mq_comm_attach / mq_comm_use: the library all-reduces the grad buffer itself
   int comm_world = 0;
@@ -442,7 +444,7 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
   plan.inline_ids = rp.nids > 0 ? 1 : 0;
   const int rw_bwd = std::min(2, pick_rw(d.R, 256));
   const int kq1 = tile_kq1(d.O);
-  const bool tiles = tiles_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused && !h->force_unfused_bwd &&
+  const bool tiles = tiles_ok(d.I, d.O, d.A, d.n, d.Tp, RT) && !h->force_unfused && !h->force_unfused_bwd &&
                      (h->row_tiles == 1 || (h->row_tiles < 0 && d.R > 512));
   const bool fused_bwd = !tiles && d.R <= h->fused_bwd_rmax && fused_bwd_ok(d.I, d.O, d.A, d.n, RT) &&
                          !h->force_unfused_bwd;
@@ -454,10 +456,11 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     pt.begin(PH_GRUF);
     const dim3 grid((d.R + TR_F - 1) / TR_F, 2);
     const float *P0 = h->on, *P1 = h->tg;
-    if (kq1 == 8) hipLaunchKernelGGL(gru_fwd_tile_kernel<8>, grid, dim3(256), 0, s, d, rp, P0, P1, L, w);
-    else if (kq1 == 20) hipLaunchKernelGGL(gru_fwd_tile_kernel<20>, grid, dim3(256), 0, s, d, rp, P0, P1, L, w);
-    else if (kq1 == 40) hipLaunchKernelGGL(gru_fwd_tile_kernel<40>, grid, dim3(256), 0, s, d, rp, P0, P1, L, w);
-    else hipLaunchKernelGGL(gru_fwd_tile_kernel<80>, grid, dim3(256), 0, s, d, rp, P0, P1, L, w);
+    if (kq1 == 8) hipLaunchKernelGGL(gru_fwd_tile_kernel<8>, grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
+    else if (kq1 == 20) hipLaunchKernelGGL(gru_fwd_tile_kernel<20>, grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
+    else if (kq1 == 40) hipLaunchKernelGGL(gru_fwd_tile_kernel<40>, grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
+    else if (kq1 == 72) hipLaunchKernelGGL(gru_fwd_tile_kernel<72>, grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
+    else hipLaunchKernelGGL(gru_fwd_tile_kernel<80>, grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
     MQ_HIP(hipGetLastError());
   } else if (rw_fwd == 1 && fused_fwd_ok(d.I, d.O, d.A, d.n, RT) && !h->force_unfused) {
     plan.fused_fwd = 1;
@@ -500,9 +503,23 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
       MQ_HIP(launch_gemm(p, (int)RT, d.A, 2, s));
     }
   }
+  h->nblk_mix = (d.M + 3) / 4;
+  bool mixed = false;   // hymix_kernel ran the mixer too
   if (c.mixer == MQ_MIXER_QMIX && !hyp_in_fwd) {
     pt.begin(PH_HYP);
-    if (hyper_ws_ok(d.S, d.E, d.NH, d.M)) {
+    if (h->hymix && hymix_ok(d.S, d.E, d.NH, d.n, d.A, d.M)) {
+      plan.hyper = MQ_HYP_MIX;
+      plan.mix = d.A <= 16 ? MQ_MIX_FAST16 : MQ_MIX_FAST32;
+      const dim3 grid((d.M + HMX_R - 1) / HMX_R);
+      if (d.A <= 16)
+        hipLaunchKernelGGL((hymix_kernel<16, 16>), grid, dim3(512), 0, s, d, rp, (const float*)h->on,
+                           (const float*)h->tg, L, w, curmax);
+      else
+        hipLaunchKernelGGL((hymix_kernel<32, 16>), grid, dim3(512), 0, s, d, rp, (const float*)h->on,
+                           (const float*)h->tg, L, w, curmax);
+      MQ_HIP(hipGetLastError());
+      mixed = true;
+    } else if (hyper_ws_ok(d.S, d.E, d.NH, d.M)) {
       plan.hyper = MQ_HYP_WS;
       // wave-specialised weight streaming (hyper_kernel.hpp)
       hipLaunchKernelGGL(hyper_ws_kernel<0>, dim3((d.M + HYR - 1) / HYR, 2), dim3(HYWS_THREADS),
@@ -522,8 +539,7 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     }
   }
   pt.begin(PH_MIX);
-  h->nblk_mix = (d.M + 3) / 4;
-  {
+  if (!mixed) {
     const bool fast = d.n <= 16 && d.E <= 64;   // mix_kernel serves the rest (n > 16 or A > 32)
     plan.mix = fast && d.A <= 16 ? MQ_MIX_FAST16 : fast && d.A <= 32 ? MQ_MIX_FAST32 : MQ_MIX_GENERIC;
     if (fast && d.A <= 16)
@@ -547,10 +563,19 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     h->nsplit_fc1 = nblk;
     const int64_t l1 = (int64_t)mq::H * d.I + mq::H;
     const float* P0 = h->on;
-    if (kq1 == 8) hipLaunchKernelGGL(gru_bwd_tile_kernel<8>, dim3(nblk), dim3(256), 0, s, d, rp, P0, L, w, h->len_rnn, l1);
-    else if (kq1 == 20) hipLaunchKernelGGL(gru_bwd_tile_kernel<20>, dim3(nblk), dim3(256), 0, s, d, rp, P0, L, w, h->len_rnn, l1);
-    else if (kq1 == 40) hipLaunchKernelGGL(gru_bwd_tile_kernel<40>, dim3(nblk), dim3(256), 0, s, d, rp, P0, L, w, h->len_rnn, l1);
-    else hipLaunchKernelGGL(gru_bwd_tile_kernel<80>, dim3(nblk), dim3(256), 0, s, d, rp, P0, L, w, h->len_rnn, l1);
+    // MQ_BWD_SPLIT=1: the two-role (chain / weight-gradient waves) variant, 512 threads
+    const bool split = getenv("MQ_BWD_SPLIT") && atoi(getenv("MQ_BWD_SPLIT")) == 1;
+#define MQ_BWD_TILE(K)                                                                                          \
+  if (split)                                                                                                    \
+    hipLaunchKernelGGL(gru_bwd_split_kernel<K>, dim3(nblk), dim3(512), 0, s, d, rp, P0, L, w, h->len_rnn, l1); \
+  else                                                                                                          \
+    hipLaunchKernelGGL(gru_bwd_tile_kernel<K>, dim3(nblk), dim3(256), 0, s, d, rp, P0, L, w, h->len_rnn, l1);
+    if (kq1 == 8) { MQ_BWD_TILE(8) }
+    else if (kq1 == 20) { MQ_BWD_TILE(20) }
+    else if (kq1 == 40) { MQ_BWD_TILE(40) }
+    else if (kq1 == 72) { MQ_BWD_TILE(72) }
+    else { MQ_BWD_TILE(80) }
+#undef MQ_BWD_TILE
     MQ_HIP(hipGetLastError());
   } else if (fused_bwd) {
     // one row per workgroup: dW_hh / dW_ih / dX1 / dW1 on the chain's idle matrix cores (gru_bwd_fused.hpp)

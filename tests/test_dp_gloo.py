@@ -139,6 +139,7 @@ def _contract_worker(rank, world, port, out_path):
         except _lib.MQError:
             res["cpu_train"] = "raised"
     finally:
+        dist.barrier()   # no rank tears gloo down while its peer is still in the last collective
         dist.destroy_process_group()
     np.save(out_path.format(rank), np.array([json.dumps(res)]))
 

@@ -456,6 +456,34 @@ def test_data_parallel_norm_path_single_rank(cases):
     assert abs(outs[1][1] - outs[0][1]) <= 1e-5 * abs(outs[0][1])
 
 
+@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_qmix_ragged", "cfg2_qmix_nodq", "cfg1_qmix", "tiny_qmix_full",
+                                  "rw2_qmix"])
+def test_hymix_bitwise(cases, name, monkeypatch):
+    """The QMIX hypernet and mixer in one launch (hymix_kernel, MQ_HYMIX=1) equal hyper_ws_kernel followed by
+    mix_fast_kernel (the default, MQ_HYMIX=0) bit for bit: parameters, gradients, square_avg, stats and the double-Q
+    actions over up to four steps (ragged episodes, double_q False, M not a multiple of 16, the row-tile agent)."""
+    from tests.gpu_helpers import build, flat_grads, flat_params
+    case = get_case(cases, name)
+    monkeypatch.setenv("MQ_HYP_IN_FWD", "0")
+    outs = []
+    for hm in ("1", "0"):
+        monkeypatch.setenv("MQ_HYMIX", hm)
+        args, buf, mac, learner, logger = build(case)
+        np.random.seed(case.sampler_seed)
+        for k in range(min(4, len(case.episodes))):
+            batch = buf.sample(case.B)
+            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
+        th.cuda.synchronize()
+        assert learner.last_plan()["hyper"] == ("ws_mix" if hm == "1" else "ws"), learner.last_plan()
+        outs.append((flat_params(learner), flat_grads(learner), learner._sq.cpu().numpy(), learner.last_stats(),
+                     learner.last_cur_max_actions().cpu().numpy()))
+    for a, b in zip(outs[0], outs[1]):
+        if isinstance(a, dict):
+            assert a == b
+        else:
+            assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg4_qmix", "cfg1_qmix", "tiny_qmix_full", "cfg2_qmix_ragged"])
 def test_hyper_in_forward_grid_bitwise(cases, name, monkeypatch):
     """The QMIX hypernet as workgroups appended to the fused forward's grid (MQ_HYP_IN_FWD=1; the default for shards
@@ -464,6 +492,7 @@ def test_hyper_in_forward_grid_bitwise(cases, name, monkeypatch):
     two-wave forward of configs[3]'s shard (cfg4) included."""
     from tests.gpu_helpers import build, flat_grads, flat_params
     case = get_case(cases, name)
+    monkeypatch.setenv("MQ_HYMIX", "0")   # both arms feed mix_fast_kernel from HYP
     outs = []
     for inf in ("1", "0"):
         monkeypatch.setenv("MQ_HYP_IN_FWD", inf)
