@@ -45,7 +45,7 @@ MQ_DEV float sigm_fast(float x) {   // 1 / (1 + e^-x) with v_exp_f32 / v_rcp_f32
 }
 
 // ------------------------------------------------------------------------------------------------ forward
-// VAR: ablation bits for scripts/rec_micro.hip only (production = 0): 1 skip Hs/Gates stores,
+// VAR: ablation bits for the round-3 scripts/rec_micro.hip only (production = 0): 1 skip Hs/Gates stores,
 // 2 stamp the T loop (cycles, 100 MHz ticks) into w.slab_mix.
 template <int RW, bool ONLINE, int VAR>
 MQ_DEV void gru_fwd_body(const Dims& d, const float* __restrict__ P, const Lay& L, const Work& w, int z) {

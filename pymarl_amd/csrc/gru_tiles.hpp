@@ -5,10 +5,11 @@
 //
 // rnn_agent.py:27-36 (fc1 -> relu -> GRUCell -> fc2) and its backward (q_learner.py:100-101), per workgroup of rows:
 //
-// Forward, gru_fwd_tile_kernel: one workgroup = 32 rows (two 16-row MFMA M-tiles) of one net (blockIdx.y), 256
-// threads. Wave w owns hidden units 16w .. 16w + 15: the N-tile w of fc1 and fc2 and the gate columns {w, 4 + w,
-// 8 + w} (r, z, n of its units) of the two 192-wide products, so the GRU gate math is lane-local. Per step t, one
-// LDS barrier, and the step's work is software-pipelined across steps:
+// Forward, gru_fwd_tile_kernel: one workgroup = 32 rows (two 16-row MFMA M-tiles) of one net, 512 threads in two
+// roles (recurrence waves 0-3, projection waves 4-7). Waves w and w + 4 own hidden units 16 (w & 3) .. + 15: the
+// N-tile of fc1 and fc2 and the gate columns {w, 4 + w, 8 + w} (r, z, n of its units) of the two 192-wide products,
+// so the GRU gate math is lane-local. Per step t, one LDS barrier, and the step's work is software-pipelined across
+// steps:
 //   GH_t  = h_{t-1} W_hh^T              [32 x 64] x [64 x 192]   (the serial part)
 //   gates -> h_t (LDS, + Hs / Gates for the BPTT when online; the tile path's Gates record is [RT][H][4] =
 //   (r, z, n, W_hn h + b_hn) per unit, one 16-byte store / load per (row, unit))
@@ -20,7 +21,8 @@
 // gathered from LDS. v_mfma_f32_16x16x4_f32 throughout (fp32 in, fp32 accumulate: the reference's arithmetic).
 //
 // Backward, gru_bwd_tile_kernel (online net): one workgroup = 16 rows, 256 threads, wave w again owns units
-// 16w .. 16w + 15. Per step t (descending), two LDS barriers:
+// 16w .. 16w + 15 (gru_bwd_split_kernel: the same step on 512 threads, chain and weight-gradient roles). Per step t
+// (descending), two LDS barriers:
 //   dh = carry + dchosen W2[a_t];  dgi, dgh from the stored gates (lane-local, as the forward's gate math)
 //   carry_{t-1} = dh z + dgh W_hh         [16 x 192] x [192 x 64]
 //   dX1 = (dgi W_ih) o [X1 > 0]           [16 x 192] x [192 x 64]
@@ -69,25 +71,31 @@ struct FwdTileLds {
   int agent[TR_F];                  // agent index of each row (the agent-id one-hot)
 };
 
-// grid = (ceil(R / 32), 2 nets), 512 threads: two waves per SIMD with split roles. Waves 0-3 run the recurrence
-// (GH, the gate math, GI; W_hh and W_ih in registers), waves 4-7 the projections (fc1 with the obs staging, fc2; W1's
-// obs part and W2 in registers). Wave w and wave w + 4 share a SIMD and own the same 16 units, so each SIMD
-// interleaves a recurrence stream (192 MFMAs a step) with a projection stream (176): one wave's LDS and MFMA
-// latencies are covered by the other's issue, and neither wave has to hold the other's 88-96 weight registers.
-// Each role is its own T loop; both pass the same barriers (one per step).
+// grid = 16 ceil(ceil(R / 32) / 8) (row tiles x 2 nets, XCD-paired), 512 threads: two waves per SIMD with split
+// roles. Waves 0-3 run the recurrence (GH, the gate math, GI; W_hh and W_ih in registers), waves 4-7 the projections
+// (fc1 with the obs staging, fc2; W1's obs part and W2 in registers). Wave w and wave w + 4 share a SIMD and own the
+// same 16 units, so each SIMD interleaves a recurrence stream (192 MFMAs a step) with a projection stream (176): one
+// wave's LDS and MFMA latencies are covered by the other's issue, and neither wave has to hold the other's 88-96
+// weight registers. Each role is its own T loop; both pass the same barriers (one per step).
 template <int KQ1>
 __global__ __launch_bounds__(512, 1) void gru_fwd_tile_kernel(Dims d, Rep rp, const float* __restrict__ P0,
                                                               const float* __restrict__ P1, Lay L, Work w) {
   __shared__ FwdTileLds<KQ1> S;
   constexpr int NS = (4 * KQ1 + 63) / 64;   // obs gather slots per lane and row
-  const int z = blockIdx.y;
+  // 1-D grid in groups of 16: block 16 k + 8 n + i is row tile 8 k + i of net n, so the two nets' workgroups of a
+  // row tile are blocks b and b + 8, which the dispatcher deals to the same XCD: the second net's obs gather hits the
+  // L2 lines the first net's brought in
+  const int nx = (d.R + TR_F - 1) / TR_F;
+  const int xt = 8 * (blockIdx.x >> 4) + (blockIdx.x & 7);
+  if (xt >= nx) return;
+  const int z = (blockIdx.x >> 3) & 1;
   const bool online = z == 0;
   const float* __restrict__ P = z ? P1 : P0;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ub = wv & 3;   // this wave's unit block
   const int R = d.R, Tp = d.Tp, O = d.O, A = d.A, n = d.n, I = d.I;
-  const int r0 = blockIdx.x * TR_F;
+  const int r0 = xt * TR_F;
   const int j = 16 * ub + c;   // this lane's hidden unit in the D layout
   const uint32_t RH = (uint32_t)R * H;
 

@@ -37,7 +37,7 @@ inline bool hyper_ok(int S, int NH) {
   return S <= 4 * HYW && NH <= 1024 && HyperGeom(S, NH).floats() * sizeof(float) <= 160 * 1024;
 }
 
-// grid = (ceil(M / 32), 2 nets), 64 * NW threads (NW = 4 or 8 waves). VAR (scripts/rec_micro.hip only): 1 stamp
+// grid = (ceil(M / 32), 2 nets), 64 * NW threads (NW = 4 or 8 waves). VAR (the round-3 scripts/rec_micro.hip only): 1 stamp
 // phases into S0[]. With 8 waves each wave owns one (16-row M-tile, 16-column N-tile) pair of a chunk; with 4 waves,
 // one N-tile for both M-tiles.
 template <int VAR = 0, int NW = 4>
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(64 * NW) void hyper_kernel(Dims d, Rep rp, const fl
 // and 8 MFMA waves (wave 4 + w: M-tile w >> 2, N-tile w & 3 of each 64-row chunk) in one 768-thread workgroup.
 // The loaders stage chunk c + 1 into the idle LDS buffer and fetch chunk c + 2 while the MFMA waves consume chunk
 // c: one barrier per chunk. gfx950 issues no VALU op while the SIMD's f32 MFMA pipe is busy
-// (scripts/coexec2_micro.hip: 48 v_fma 56 -> 564 cycles beside MFMA chains), so the loader path carries no VALU
+// (scripts/coexec2_micro.hip, in git at 2f3e4ef: 48 v_fma 56 -> 564 cycles beside MFMA chains), so the loader path carries no VALU
 // and no branch: loader wave lw copies the 16 contiguous weight rows 16 (4c + lw) .. + 15 (one parameter segment
 // when E % 16 == 0) as 48 x 64 floats (buffer loads: scalar row-group base, lane offset 4 lane + 256 q; past the
 // group they read the following parameters, past the end zeros) into a 3072-float LDS slot (row pitch S, ds_write

@@ -454,7 +454,7 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
   if (tiles) {
     // row tiles of 32 (two M-tiles) per workgroup, both nets: the recurrence and fc1 / W_ih / fc2 on MFMA
     pt.begin(PH_GRUF);
-    const dim3 grid((d.R + TR_F - 1) / TR_F, 2);
+    const dim3 grid(16 * (((d.R + TR_F - 1) / TR_F + 7) / 8));   // row tiles x 2 nets, XCD-paired (gru_tiles.hpp)
     const float *P0 = h->on, *P1 = h->tg;
     if (kq1 == 8) hipLaunchKernelGGL(gru_fwd_tile_kernel<8>, grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
     else if (kq1 == 20) hipLaunchKernelGGL(gru_fwd_tile_kernel<20>, grid, dim3(512), 0, s, d, rp, P0, P1, L, w);
@@ -563,8 +563,8 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     h->nsplit_fc1 = nblk;
     const int64_t l1 = (int64_t)mq::H * d.I + mq::H;
     const float* P0 = h->on;
-    // MQ_BWD_SPLIT=1: the two-role (chain / weight-gradient waves) variant, 512 threads
-    const bool split = getenv("MQ_BWD_SPLIT") && atoi(getenv("MQ_BWD_SPLIT")) == 1;
+    // the two-role (chain / weight-gradient waves) BPTT, 512 threads; MQ_BWD_SPLIT=0: one wave per SIMD, 256 threads
+    const bool split = !(getenv("MQ_BWD_SPLIT") && atoi(getenv("MQ_BWD_SPLIT")) == 0);
 #define MQ_BWD_TILE(K)                                                                                          \
   if (split)                                                                                                    \
     hipLaunchKernelGGL(gru_bwd_split_kernel<K>, dim3(nblk), dim3(512), 0, s, d, rp, P0, L, w, h->len_rnn, l1); \

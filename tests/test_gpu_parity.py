@@ -344,7 +344,10 @@ UNFUSED_ENV = ("MQ_UNFUSED_FWD", "MQ_UNFUSED_BWD")
     ("tiny_qmix_nodq", 4, False), ("tiny_qmix_nola", 4, False), ("tiny_vdn_noid", 4, False),
     ("tiny_qmix_bare", 4, False), ("cfg2_qmix_nodq", 5, False), ("cfg1_qmix", 10, False), ("cfg1_vdn", 5, False)])
 def test_teacher_forced_steps(cases, name, steps, unfused, monkeypatch):
-    run_teacher_forced(get_case(cases, name), steps, unfused, monkeypatch)
+    learner = run_teacher_forced(get_case(cases, name), steps, unfused, monkeypatch)
+    if name == "cfg3_vdn_b128":   # BASELINE configs[2] itself: the bench's plan (row tiles, no fused kernels)
+        plan = learner.last_plan()
+        assert plan["tiles"] == 1 and plan["fused_fwd"] == 0 and plan["fused_bwd"] == 0, plan
 
 
 @pytest.mark.parametrize("name,steps,flow", [
