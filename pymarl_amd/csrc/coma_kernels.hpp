@@ -177,7 +177,7 @@ using CLinProb = CLinProbT<128>;
 // in torch's evaluation order without FMA contraction. Writes targets [T][R]. LDS: Tp * (n + 3) floats.
 __global__ __launch_bounds__(256) void coma_td_kernel(CDims d, Rep rp, const float* __restrict__ Qt,
                                                       float* __restrict__ tgt) {
-  extern __shared__ float sm[];
+  extern __shared__ __attribute__((aligned(16))) float sm[];
   const int b = blockIdx.x, n = d.n, Tp = d.Tp;
   float* tq = sm;              // [Tp][n]
   float* rw = tq + Tp * n;     // [Tp]
@@ -355,7 +355,7 @@ __host__ __device__ inline int l1_slices(int Kp) { return (Kp + KW - 1) / KW; }
 __global__ __launch_bounds__(256) void coma_l1_kernel(CritArgs a, int t, int Lexp) {
   const float mt = a.msum[t];
   const int L = a.cstate[0];
-  extern __shared__ float sm[];
+  extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int WP = KW + 1;
   const int Kp = a.d.Kp, Kc = a.d.Kc, R = a.d.R;
   const int ks = blockIdx.x, u0 = blockIdx.y * 16, rbase = blockIdx.z * kL1Rows;
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(256) void coma_l1_kernel(CritArgs a, int t, int Lex
 __global__ __launch_bounds__(kHeadThreads) void coma_head_kernel(CritArgs a, int t, int Lexp) {
   const float mt = a.msum[t];
   const int L = a.cstate[0];
-  extern __shared__ float sm[];
+  extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int CP = CH + 1;
   const int A = a.d.A, A16 = (A + 15) / 16 * 16, R = a.d.R, n = a.d.n;
   float* W2s = sm;                 // [CH][CP]

@@ -27,7 +27,7 @@ namespace mq {
 
 constexpr int BRP = 4 * H + 4;   // history row pitch: [dgh | h_{t-1}] and [dgi | -], padded against bank conflicts
 
-struct BwdFusedLds {
+struct alignas(16) BwdFusedLds {
   float gh[2][FCH][BRP];     // per step: dgh (3H) | h_{t-1} (H), chunk-double-buffered
   float gi[2][FCH][BRP];     // per step: dgi (3H) | unused
   float x1[FCH][H + 4];      // X1 of the chunk being reduced

@@ -46,7 +46,7 @@ inline bool fused_fwd_ok(int I, int O, int A, int n, int64_t RT) {
   return I <= 4 * FKQ && O <= 128 && A <= 16 && n * O < (1 << 16) && RT * I < (int64_t(1) << 31);
 }
 
-struct FusedLds {
+struct alignas(16) FusedLds {
   float h0[H];               // init_hidden: zeros (the h_{t-1} of step 0)
   float hs[2][FCH][H + 4];   // h of the last two chunks: the recurrence's h_{t-1} and fc2's operand
   float gi[2][FCH][G3];      // input gates of the current / next chunk

@@ -35,7 +35,8 @@
 //
 // MFMA operand maps (v_mfma_f32_16x16x4_f32, lane l, g = l >> 4, c = l & 15): A[i = c][kk = g], B[kk = g][j = c],
 // D[i = 4g + e][j = c]. Where K is a feature dimension, lane group g owns a contiguous quarter of it (k = Kq g + s),
-// so A and B fragments are b128 reads; where K is the 16 rows of a tile, k = 4 s + g.
+// so A and B fragments are b128 reads; where K is the 16 rows of a tile, lane group g takes rows 4 g .. 4 g + 3
+// (k = 4 g + s: with the tiles' row pitches = 4 mod 64 banks, the 64 lanes' scalar operand reads hit 64 banks).
 #pragma once
 #include "gru_kernels.hpp"
 #include "gru_fwd_fused.hpp"
@@ -62,7 +63,7 @@ inline bool tiles_ok(int I, int O, int A, int n, int Tp, int64_t RT) {
 }
 
 template <int KQ1>
-struct FwdTileLds {
+struct alignas(16) FwdTileLds {
   float xo[2][TR_F][4 * KQ1 + 4];   // obs rows of steps t + 2 / t + 3 (zero past O)
   float hb[2][TR_F][T_HP];          // h_{t-1} / h_t
   float x1[2][TR_F][T_HP];          // X1 of steps t + 1 / t + 2
@@ -357,7 +358,7 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_tile_kernel(Dims d, Rep rp, co
 
 // ------------------------------------------------------------------------------------------------ backward
 template <int KQ1>
-struct BwdTileLds {
+struct alignas(16) BwdTileLds {
   float dgh[TR_B][G3 + 4];        // the step's dgh = [da_r | da_z | da_n r]
   float dgi[TR_B][G3 + 4];        // the step's dgi = [da_r | da_z | da_n]
   float hb[3][TR_B][T_HP];        // h_tau in hb[tau % 3]: h_{t-1} (dW_hh) and h_t (dW2) of step t
@@ -582,12 +583,12 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_tile_kernel(Dims d, Rep rp, co
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    // dW_hh += dgh^T h_{t-1}, dW_ih += dgi^T X1 (K = the 16 rows, k = 4 s + g)
+    // dW_hh += dgh^T h_{t-1}, dW_ih += dgi^T X1 (K = the 16 rows, k = 4 g + s)
     {
       const int hbuf = (t + 2) % 3;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const int row = 4 * s + g;
+        const int row = 4 * g + s;
         float a_h[3], a_i[3], b_h[4], b_x[4];
 #pragma unroll
         for (int m = 0; m < 3; ++m) {
@@ -614,7 +615,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_tile_kernel(Dims d, Rep rp, co
       const float(*xi)[16 * T_NI + 4] = S.xin[t & 1];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const int row = 4 * s + g;
+        const int row = 4 * g + s;
         const float av = S.dx1[row][j];
 #pragma unroll
         for (int q = 0; q < T_NI; ++q)
@@ -623,7 +624,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_tile_kernel(Dims d, Rep rp, co
       const int hbuf = t % 3;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const int row = 4 * s + g;
+        const int row = 4 * g + s;
         const float dchv = S.dchs[t & 3][row];
         const int aw = S.acts[t & 3][row];
         const float bv = S.hb[hbuf][row][j];
@@ -631,7 +632,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_tile_kernel(Dims d, Rep rp, co
         for (int m = 0; m < 3; ++m) {
           const float av = aw == 16 * m + c ? dchv : 0.0f;
           acc_w2[m] = mfma16x4(av, bv, acc_w2[m]);
-          if (ub == 0) db2[m] += av;   // rows 4 s + g of this lane group; the groups are summed at the end
+          if (ub == 0) db2[m] += av;   // rows 4 g + s of this lane group; the groups are summed at the end
         }
       }
     }
@@ -667,7 +668,7 @@ __global__ __launch_bounds__(256, 1) void gru_bwd_tile_kernel(Dims d, Rep rp, co
       const int a = 16 * m + 4 * g + e;
       if (a < A) slab[o_w2 + a * H + j] = acc_w2[m][e];
     }
-  // bias gradients: this lane's partials cover rows 4 g .. 4 g + 3 (db2: rows 4 s + g); sum the four lane groups
+  // bias gradients: this lane's partials cover rows 4 g .. 4 g + 3 (db2 too); sum the four lane groups
   auto gsum = [](float v) {
     v += __shfl_xor(v, 16, 64);
     return v + __shfl_xor(v, 32, 64);
@@ -729,19 +730,19 @@ __global__ __launch_bounds__(512, 1) void gru_bwd_split_kernel(Dims d, Rep rp, c
   float* slab1 = w.slab_fc1 + (int64_t)blockIdx.x * slab1_len;
   const int64_t o_hh = L.o[MQ_P_RNN_W_HH] - base, o_bi = L.o[MQ_P_RNN_B_IH] - base,
                 o_bh = L.o[MQ_P_RNN_B_HH] - base, o_w2 = L.o[MQ_P_FC2_W] - base, o_b2 = L.o[MQ_P_FC2_B] - base;
-  // bias gradients: a lane's partials cover rows 4 g .. 4 g + 3 (db2: rows 4 s + g); sum the four lane groups
+  // bias gradients: a lane's partials cover rows 4 g .. 4 g + 3 (db2 too); sum the four lane groups
   auto gsum = [](float v) {
     v += __shfl_xor(v, 16, 64);
     return v + __shfl_xor(v, 32, 64);
   };
   // dW1 += dX1^T xin_t over column tiles q0 + [0, NQ) below q1, in pairs (a pair starting past NI is skipped; a
-  // pair's second tile past NI is computed and never written out) (K = the 16 rows, k = 4 s + g)
+  // pair's second tile past NI is computed and never written out) (K = the 16 rows, k = 4 g + s)
   auto dw1_tiles = [&](int t, auto& acc, int q0, int q1) {
     constexpr int NQ = sizeof(acc) / sizeof(acc[0]);
     const float(*xi)[16 * T_NI + 4] = S.xin[t & 1];
     float av[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) av[s] = S.dx1[4 * s + g][j];
+    for (int s = 0; s < 4; ++s) av[s] = S.dx1[4 * g + s][j];
 #pragma unroll
     for (int qp = 0; qp < NQ; qp += 2) {
       if (q0 + qp < q1) {
@@ -749,7 +750,7 @@ __global__ __launch_bounds__(512, 1) void gru_bwd_split_kernel(Dims d, Rep rp, c
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
-          for (int u = 0; u < 2; ++u) bv[s][u] = xi[4 * s + g][16 * (q0 + qp + u) + c];
+          for (int u = 0; u < 2; ++u) bv[s][u] = xi[4 * g + s][16 * (q0 + qp + u) + c];
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -991,12 +992,12 @@ __global__ __launch_bounds__(512, 1) void gru_bwd_split_kernel(Dims d, Rep rp, c
           db1 += v;
         }
       }
-      // dW_hh += dgh^T h_{t-1}, dW_ih += dgi^T X1 (K = the 16 rows, k = 4 s + g)
+      // dW_hh += dgh^T h_{t-1}, dW_ih += dgi^T X1 (K = the 16 rows, k = 4 g + s)
       {
         const int hbuf = (t + 2) % 3;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const int row = 4 * s + g;
+          const int row = 4 * g + s;
           float a_h[3], a_i[3], b_h[4], b_x[4];
 #pragma unroll
           for (int m = 0; m < 3; ++m) {
@@ -1024,7 +1025,7 @@ __global__ __launch_bounds__(512, 1) void gru_bwd_split_kernel(Dims d, Rep rp, c
         const int hbuf = t % 3;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const int row = 4 * s + g;
+          const int row = 4 * g + s;
           const float dchv = S.dchs[t & 3][row];
           const int aw = S.acts[t & 3][row];
           const float bv = S.hb[hbuf][row][j];
@@ -1032,7 +1033,7 @@ __global__ __launch_bounds__(512, 1) void gru_bwd_split_kernel(Dims d, Rep rp, c
           for (int m = 0; m < 3; ++m) {
             const float av = aw == 16 * m + c ? dchv : 0.0f;
             acc_w2[m] = mfma16x4(av, bv, acc_w2[m]);
-            if (ub == 0) db2[m] += av;   // rows 4 s + g of this lane group; the groups are summed at the end
+            if (ub == 0) db2[m] += av;   // rows 4 g + s of this lane group; the groups are summed at the end
           }
         }
       }

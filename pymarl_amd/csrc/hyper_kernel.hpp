@@ -46,7 +46,7 @@ __global__ __launch_bounds__(64 * NW) void hyper_kernel(Dims d, Rep rp, const fl
                                                         float* __restrict__ S0) {
   constexpr int NT = 64 * NW, WR = 64 / NW, SR = HYR / NW;   // threads, weight rows / state rows per wave
   uint64_t ts0 = (VAR & 1) ? __builtin_amdgcn_s_memtime() : 0, tstore = 0, tbar = 0, tmfma = 0, tfetch = 0, tg = 0;
-  extern __shared__ float dyn[];
+  extern __shared__ __attribute__((aligned(16))) float dyn[];
   const HyperGeom G(d.S, d.NH);
   float* st = dyn;                  // [32][SP] gathered states, zero-padded
   float* wst = st + HYR * G.SP;     // [2][64][SP] weight chunks (double-buffered)
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(HYWS_THREADS) void hyper_ws_kernel(Dims d, Rep rp, 
                                                                 float* __restrict__ HYP, float* __restrict__ S0) {
   constexpr int NLW = 4, SR = HYR / 8, SP = HYWS_SPS, HCG = HYW / 16;
   const uint64_t ts0 = (VAR & 1) ? __builtin_amdgcn_s_memtime() : 0;
-  extern __shared__ float dyn[];
+  extern __shared__ __attribute__((aligned(16))) float dyn[];
   const int S = d.S, NH = d.NH, n = d.n, E = d.E;
   const int Kq = HYW, NCH = (NH + 63) / 64, WB = 4 * HYWS_GS;   // fixed K extent: 4 Kq = 192 >= S
   float* st = dyn;                  // [32][SP] gathered states, zero K-padding
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(HYWS_THREADS) void hyper_ws_kernel(Dims d, Rep rp, 
 constexpr int HMX_R = 16;
 constexpr int HMX_NHP = 452;   // LDS pitch of a HYP row: NH <= 448
 template <int MN>
-struct HymixLds {
+struct alignas(16) HymixLds {
   float hyp[2][HMX_R][HMX_NHP];
   MixScratch<MN> sc[8];
   float red[HMX_R][8];

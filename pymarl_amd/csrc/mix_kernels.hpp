@@ -228,7 +228,7 @@ namespace mq {
 // land in red_slot[0..4] / v2_slot[0..64] for the caller's fixed-order block sums. Two workgroup barriers inside:
 // every wave of the workgroup must call it the same number of times.
 template <int MN>
-struct MixScratch {
+struct alignas(16) MixScratch {
   float chs[64], tms[64], dps[64];
   float w1s[MN][65];   // |hyper_w_1| rows of the online mixer, for dLoss/dchosen
 };

@@ -28,7 +28,7 @@ inline size_t qmix_forward_lds(int n, int S, int E) {
 __global__ __launch_bounds__(256) void qmix_forward_kernel(const float* __restrict__ W, int n, int S, int E,
                                                            const float* __restrict__ qs, const float* __restrict__ st,
                                                            float* __restrict__ out, int rows) {
-  extern __shared__ float lds[];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
   const int NH = E * (n + 3);
   float* s_st = lds;                       // [QMF_ROWS][S]
   float* s_h = lds + QMF_ROWS * S;         // [QMF_ROWS][NH]

@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void mac_step_kernel(Dims d, Rep rp, const flo
                                                        const float* __restrict__ xin_dense,
                                                        const float* __restrict__ h_in, float* __restrict__ h_out,
                                                        float* __restrict__ q_out) {
-  extern __shared__ float sm[];   // xin [I] | x1 [H] | h [H] | gi [3H] | gh [3H] | h1 [H]
+  extern __shared__ __attribute__((aligned(16))) float sm[];   // xin [I] | x1 [H] | h [H] | gi [3H] | gh [3H] | h1 [H]
   float* xin = sm;
   float* x1 = xin + ((d.I + 3) & ~3);
   float* hh = x1 + H;
