@@ -344,6 +344,10 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_tile_kernel(Dims d, Rep rp, co
     stage_obs(2);    // xo[0]: fc1(0) has read it
     issue_obs(3);
     lds_barrier();   // #3
+    // the projection waves (the younger half) at priority 1: they otherwise lose every issue arbitration to the
+    // recurrence waves, and the step waits on their fc1 (r04r: forward 1.33 -> 1.28 ms; the BPTT's weight-gradient
+    // waves measured slower with it)
+    __builtin_amdgcn_s_setprio(1);
     for (int t = 0; t < Tp; ++t) {
       // obs of step t + 3 into xo[(t + 3) & 1] (fc1(t + 1) read it in step t - 1), then step t + 4's loads
       stage_obs(t + 3);
