@@ -362,32 +362,19 @@ __global__ __launch_bounds__(512) void hymix_kernel(Dims d, Rep rp, const float*
     }
     // ---- B operand: weight rows j0 + c16 of the tile's segment, K quarter g: each lane's 48 K values are contiguous,
     // 12 dwordx4 buffer loads through the parameter descriptor (past the buffer: 0; past S within a row: the next
-    // row's finite values, times the zero A padding) plus the bias. The loads are issued as inline asm with explicit
-    // vmcnt waits, so the next tile's 13 loads stay in flight under the current tile's 48 MFMAs (the compiler's own
-    // wait counting across the tile loop waits for both sets).
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const uint64_t pa = (uint64_t)(uintptr_t)P;
-    const u32x4 rsrc = {(uint32_t)pa, (uint32_t)(pa >> 32), (uint32_t)(L.o[MQ_P_COUNT] * sizeof(float)), 0x00020000u};
+    // row's finite values, times the zero A padding) plus the bias; two register sets with compile-time names (the
+    // tile loop is unrolled by two), so the next tile's loads are in flight under the current tile's 48 MFMAs
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)P, (short)0, (int)(L.o[MQ_P_COUNT] * sizeof(float)), 0x00020000);
     f32x4 bwa[12], bwb[12];
     float bja = 0.0f, bjb = 0.0f;
     auto fetch = [&](int nt, f32x4 (&dst)[12], float& bj) {
       const HypSeg sg = hyp_seg(L, n * E, E, 16 * nt);
-      const uint32_t base = (uint32_t)((sg.w + (int64_t)(sg.row + c16) * Sd + 48 * g) * 4);
+      const int base = (int)((sg.w + (int64_t)(sg.row + c16) * Sd + 48 * g) * 4);
 #pragma unroll
       for (int q = 0; q < 12; ++q)
-        asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3"
-                     : "=v"(dst[q]) : "v"(base), "s"(rsrc), "i"(16 * q) : "memory");
-      const uint32_t boff = (uint32_t)((sg.b + sg.row + c16) * 4);
-      asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(bj) : "v"(boff), "s"(rsrc) : "memory");
-    };
-    // wait until at most `pending` of this wave's loads are outstanding, then hand the tile's registers to the
-    // compiler (the empty asm ties every use behind the wait)
-    auto ready = [&](f32x4 (&bw)[12], float& bj, bool pending) {
-      if (pending) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int q = 0; q < 12; ++q) asm volatile("" : "+v"(bw[q]));
-      asm volatile("" : "+v"(bj));
+        dst[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, base + 16 * q, 0, 0));
+      bj = P[sg.b + sg.row + c16];
     };
     auto tile = [&](int nt, const f32x4 (&bw)[12], float bj) {
       f32x4 acc = {0, 0, 0, 0};
@@ -398,23 +385,17 @@ __global__ __launch_bounds__(512) void hymix_kernel(Dims d, Rep rp, const float*
 #pragma unroll
       for (int e = 0; e < 4; ++e) S.hyp[z][4 * g + e][16 * nt + c16] = acc[e] + bj;
     };
-    // the state rows' loads (and S0's stores) are the compiler's: drain them before the counted loads start
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-#if defined(MQ_HYMIX_EXP) && MQ_HYMIX_EXP == 2
+#if defined(MQ_HYMIX_EXP) && MQ_HYMIX_EXP == 2   // diagnostic build: the mixer part alone (r04n)
     int nt = NT;
 #else
     int nt = wl;
 #endif
     if (nt < NT) fetch(nt, bwa, bja);
     for (; nt < NT; nt += 8) {
-      const bool nb = nt + 4 < NT;
-      if (nb) fetch(nt + 4, bwb, bjb);
-      ready(bwa, bja, nb);
+      if (nt + 4 < NT) fetch(nt + 4, bwb, bjb);
       tile(nt, bwa, bja);
-      if (!nb) break;
-      const bool na = nt + 8 < NT;
-      if (na) fetch(nt + 8, bwa, bja);
-      ready(bwb, bjb, na);
+      if (nt + 4 >= NT) break;
+      if (nt + 8 < NT) fetch(nt + 8, bwa, bja);
       tile(nt + 4, bwb, bjb);
     }
   }
