@@ -533,6 +533,7 @@ def main():
     th.cuda.synchronize()
     survey = learner.phase_times()
     dominant = max(survey, key=survey.get)
+    plan = learner.last_plan()   # the kernel variants the timed steps run (row tiles, fused kernels, hypernet, mixer)
     fused_fwd = survey.get("fc1", 0.0) == 0.0     # the fused agent forward carries fc1 / W_ih / fc2
     fused_bwd = survey.get("dx1", 0.0) == 0.0     # the fused BPTT carries dX1 / dW1
 
@@ -570,7 +571,7 @@ def main():
         roof = {"bound": "mfma", "kernel": dominant, "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": (achieved / FP32_PEAK_TFLOPS) if achieved else None,
                 "traffic": traffic, "traffic_source": traffic_src, "launch_ms": dom_ms, "flops_per_launch": fl,
-                "fused": {"fwd": fused_fwd, "bwd": fused_bwd}}
+                "fused": {"fwd": fused_fwd, "bwd": fused_bwd}, "plan": plan}
         cpu = rollout = None
         if world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(a.config, data)
