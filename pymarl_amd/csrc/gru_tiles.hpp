@@ -166,7 +166,9 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_tile_kernel(Dims d, Rep rp, co
     lds_barrier();   // #3
     float hprev[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     const auto hsb = buf_rsrc(w.Hs);
-    for (int t = 0; t < Tp; ++t) {
+    // one step: the input gates of step t in gi_t (registers), those of step t + 1 into gi_n. The loop runs two steps
+    // per iteration with the two sets swapping roles, so no register copy carries GI across the back edge.
+    auto step = [&](int t, const f32x4 (&gi_t)[2][3], f32x4 (&gi_n)[2][3]) {
       // GH_t = h_{t-1} W_hh^T
       f32x4 gh[2][3];
       prod3(S.hb[(t + 1) & 1], whh, gh);
@@ -178,10 +180,10 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_tile_kernel(Dims d, Rep rp, co
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = 16 * mt + 4 * g + e, r = r0 + i;
-          const float rg = sigm_fast((gh[mt][0][e] + bhr) + (gi[mt][0][e] + bir));
-          const float zg = sigm_fast((gh[mt][1][e] + bhz) + (gi[mt][1][e] + biz));
+          const float rg = sigm_fast((gh[mt][0][e] + bhr) + (gi_t[mt][0][e] + bir));
+          const float zg = sigm_fast((gh[mt][1][e] + bhz) + (gi_t[mt][1][e] + biz));
           const float ghn = gh[mt][2][e] + bhn;
-          const float ng = tanh_fast((gi[mt][2][e] + bin) + ghn * rg);
+          const float ng = tanh_fast((gi_t[mt][2][e] + bin) + ghn * rg);
           const float h1 = (hprev[mt][e] - ng) * zg + ng;
           hprev[mt][e] = h1;
           S.hb[t & 1][i][j] = h1;
@@ -190,9 +192,16 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_tile_kernel(Dims d, Rep rp, co
           buf_st4(gb, st ? ((uint32_t)r * H + j) * 16 : kDrop, f32x4{rg, zg, ng, ghn});
         }
       // GI of step t + 1 (X1_{t+1}, built by the projection waves in step t - 1)
-      prod3(S.x1[(t + 1) & 1], wih, gi);
+      prod3(S.x1[(t + 1) & 1], wih, gi_n);
       lds_barrier();
+    };
+    f32x4 gi2[2][3];
+    int t = 0;
+    for (; t + 1 < Tp; t += 2) {
+      step(t, gi, gi2);
+      step(t + 1, gi2, gi);
     }
+    if (t < Tp) step(t, gi, gi2);
   } else {
     // ================================================================ projection waves
     float w1[KQ1];   // W1[j][KQ1 g + s] (obs part; zero past O)
@@ -224,16 +233,24 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_tile_kernel(Dims d, Rep rp, co
     for (int i = 0; i < 8; ++i) {
       const int r = min(r0 + 8 * ub + i, R - 1);
       const int b = (int)fdiv((uint32_t)r, d.dN), ag = r - b * n;
-      rowb[i] = rp.obs + (rp.ep(b) * d.t_stride * n + ag) * (int64_t)O;
+      const uint64_t pa = (uint64_t)(uintptr_t)(rp.obs + (rp.ep(b) * d.t_stride * n + ag) * (int64_t)O);
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pa), hi = __builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32));
+      rowb[i] = (const float*)(uintptr_t)(((uint64_t)hi << 32) | lo);   // wave-uniform: a descriptor base below
     }
+    // the obs rows go through one buffer descriptor per row and step (SGPR base, O floats long): columns past O
+    // read 0 from the range check, so neither a clamp nor a select per element is needed
     float xr[8][NS];
     auto issue_obs = [&](int t) {
+      t = __builtin_amdgcn_readfirstlane(t);   // uniform already; said so, or hipcc keeps t in a VGPR here
       const int tc = min(t, Tp - 1);
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 8; ++i) {
+        const auto ors = __builtin_amdgcn_make_buffer_rsrc((void*)(rowb[i] + (int64_t)tc * nO), (short)0, O * 4,
+                                                           0x00020000);
 #pragma unroll
         for (int s = 0; s < NS; ++s)
-          xr[i][s] = ld_u32(rowb[i] + (int64_t)tc * nO, (uint32_t)min(lane + 64 * s, O - 1));
+          xr[i][s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ors, (lane + 64 * s) * 4, 0, 0));
+      }
     };
     auto stage_obs = [&](int t) {
       const int buf = t & 1;
@@ -242,7 +259,7 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_tile_kernel(Dims d, Rep rp, co
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
           const int col = lane + 64 * s;
-          if (col < 4 * KQ1) S.xo[buf][8 * ub + i][col] = col < O ? xr[i][s] : 0.0f;
+          if (col < 4 * KQ1) S.xo[buf][8 * ub + i][col] = xr[i][s];
         }
     };
     // the agent-id one-hot term of this lane's 8 (row, unit) pairs (constant over t; read once the table is up)
@@ -782,14 +799,16 @@ __global__ __launch_bounds__(512, 1) void gru_bwd_split_kernel(Dims d, Rep rp, c
 #pragma unroll
       for (int s = 0; s < 48; ++s) whh[s] = Wh[(int64_t)(48 * g + s) * H + j];
     }
-    // obs rows 4 ub + i (wave-uniform row bases)
+    // obs rows 4 ub + i (wave-uniform row bases, made provably uniform: they become buffer descriptors below)
     const int nO = n * O;
     const float* rowb[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = row_of(4 * ub + i);
       const int b = (int)fdiv((uint32_t)r, d.dN), ag = r - b * n;
-      rowb[i] = rp.obs + (rp.ep(b) * d.t_stride * n + ag) * (int64_t)O;
+      const uint64_t pa = (uint64_t)(uintptr_t)(rp.obs + (rp.ep(b) * d.t_stride * n + ag) * (int64_t)O);
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pa), hi = __builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32));
+      rowb[i] = (const float*)(uintptr_t)(((uint64_t)hi << 32) | lo);
     }
     // lane tid < 16: row tid's action, filled and dchosen streams (staged into LDS per step)
     const int rl = row_of(tid & 15);
@@ -808,27 +827,39 @@ __global__ __launch_bounds__(512, 1) void gru_bwd_split_kernel(Dims d, Rep rp, c
     // wait for store_row, so no load result is consumed in the step that issues it)
     float dch_n = 0.0f;
     int act_n = 0, fil_n = 0, apv_n = 0, t_n = 0;
+    // the loads go through buffer descriptors with a per-step SGPR base and per-lane byte offsets fixed for the
+    // whole loop (no 64-bit address arithmetic on the chain waves' VALU, which f32 MFMA blocks)
+    uint32_t off_rj[4], off_ob[NS];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) off_rj[e] = ((uint32_t)row_of(4 * g + e) * H + j) * 4;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) off_ob[s] = (uint32_t)min(lane + 64 * s, O - 1) * 4;
     auto fetch = [&](int t, In& x) {
+      t = __builtin_amdgcn_readfirstlane(t);   // uniform already; said so, or hipcc keeps t in a VGPR here and
+                                               // waterfall-loops every descriptor built from it
       const int tc = max(t, 0), tm = max(t - 1, 0);
-      const f32x4* gbase = (const f32x4*)(w.Gates + (int64_t)tc * (4 * RH));
+      const auto grs = buf_rsrc(w.Gates + (int64_t)tc * (4 * RH));   // the tile path's [RT][H][4] gate record
+      const auto hrs = buf_rsrc(w.Hs + (int64_t)tm * RH);
+      const auto xrs = buf_rsrc(w.X1 + (int64_t)tc * RH);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int r = row_of(4 * g + e);
-        const f32x4 gv = gbase[(uint32_t)r * H + j];   // the tile path's [RT][H][4] gate record
+        const f32x4 gv = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(grs, 4 * off_rj[e], 0, 0));
         x.gr[e] = gv[0];
         x.gz[e] = gv[1];
         x.gn[e] = gv[2];
         x.ghn[e] = gv[3];
-        x.hp[e] = ld_u32(w.Hs + (int64_t)tm * RH, (uint32_t)r * H + j);
-        x.x1[e] = ld_u32(w.X1 + (int64_t)tc * RH, (uint32_t)r * H + j);
+        x.hp[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(hrs, off_rj[e], 0, 0));
+        x.x1[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, off_rj[e], 0, 0));
       }
       // obs rows of step tc (registers until stage: an LDS-DMA here would make the compiler wait for it at every
       // later LDS read of the step)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
+        const auto ors = buf_rsrc(rowb[i] + (int64_t)tc * nO);
 #pragma unroll
         for (int s = 0; s < NS; ++s)
-          x.ob[i][s] = ld_u32(rowb[i] + (int64_t)tc * nO, (uint32_t)min(lane + 64 * s, O - 1));
+          x.ob[i][s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ors, off_ob[s], 0, 0));
+      }
     };
     // row tid's dchosen and a_t of step t, and a_{t-1} (when t > 0 and slot t - 1 was filled: the last-action
     // one-hot). Rows past R (a partial last tile) get dchosen = 0: their dh, gate derivatives and every gradient
@@ -863,14 +894,13 @@ __global__ __launch_bounds__(512, 1) void gru_bwd_split_kernel(Dims d, Rep rp, c
 #pragma unroll
         for (int s = 0; s < NS; ++s)
           if (lane + 64 * s < O) xi[4 * ub + i][lane + 64 * s] = x.ob[i][s];
-      // one-hot columns [O, 16 NI) of rows 4 ub .. 4 ub + 3, zeros and ones in one pass
-      const int wd = 16 * NI - O;
-      const int* apt = S.ap[t & 3];
-      for (int e = lane; e < 4 * wd; e += 64) {
-        const int i = 4 * ub + e / wd, col = e % wd;
-        const bool one = (d.last_action && col < A && col == apt[i]) ||
-                         (d.agent_id && col == (d.last_action ? A : 0) + S.agent[i]);
-        xi[i][O + col] = one ? 1.0f : 0.0f;
+      // the last-action one-hot of rows 4 ub .. 4 ub + 3: clear the one this buffer held two steps ago (a_{t+1}, still
+      // in ring slot t + 2), set a_{t-1}'s (the agent-id ones were set in the prologue, the rest stays zero)
+      if (d.last_action && lane < 4) {
+        const int i = 4 * ub + lane;
+        const int old = S.ap[(t + 2) & 3][i], now = S.ap[t & 3][i];
+        if (old >= 0) xi[i][O + old] = 0.0f;
+        if (now >= 0) xi[i][O + now] = 1.0f;
       }
     };
 
@@ -882,11 +912,16 @@ __global__ __launch_bounds__(512, 1) void gru_bwd_split_kernel(Dims d, Rep rp, c
 
     // ---- prologue: a_{t-1} of the two top steps into the ring, step Tp - 1's inputs in registers
     In cur;
+    if (wv == 0) (&S.ap[0][0])[lane] = -1;   // the ring's a_{t-1} slots start empty (stage clears slot t + 2's)
     if (tid < TR_B) {
       fetch_row(Tp - 1);
       store_row(Tp - 1);
     }
     lds_barrier();   // the zeroed xin / hb and the ring before any stage writes
+    if (d.agent_id && lane < 8) {   // the agent-id one-hots of this wave's rows, both buffers, for the whole loop
+      const int i = 4 * ub + (lane & 3);
+      S.xin[lane >> 2][i][O + (d.last_action ? A : 0) + S.agent[i]] = 1.0f;
+    }
     if (tid < TR_B) fetch_row(Tp - 2);   // stored by the first iteration
     fetch(Tp - 1, cur);
 
