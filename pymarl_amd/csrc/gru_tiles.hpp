@@ -136,12 +136,12 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_tile_kernel(Dims d, Rep rp, co
           wih[gt][q] = *(const f32x4*)(Wi + (int64_t)(gt * H + j) * H + 16 * g + 4 * q);
         }
     }
-    const float bir = P[L.o[MQ_P_RNN_B_IH] + j], biz = P[L.o[MQ_P_RNN_B_IH] + H + j],
-                bin = P[L.o[MQ_P_RNN_B_IH] + 2 * H + j];
-    const float bhr = P[L.o[MQ_P_RNN_B_HH] + j], bhz = P[L.o[MQ_P_RNN_B_HH] + H + j],
-                bhn = P[L.o[MQ_P_RNN_B_HH] + 2 * H + j];
-    // the 192-wide product of a 32 x 64 LDS tile with a register-resident weight (A fragments read up front)
-    auto prod3 = [&](const float (*tile)[T_HP], const f32x4 (&wt)[3][4], f32x4 (&out)[2][3]) {
+    const float bi[3] = {P[L.o[MQ_P_RNN_B_IH] + j], P[L.o[MQ_P_RNN_B_IH] + H + j], P[L.o[MQ_P_RNN_B_IH] + 2 * H + j]};
+    const float bh[3] = {P[L.o[MQ_P_RNN_B_HH] + j], P[L.o[MQ_P_RNN_B_HH] + H + j], P[L.o[MQ_P_RNN_B_HH] + 2 * H + j]};
+    // the 192-wide product of a 32 x 64 LDS tile with a register-resident weight (A fragments read up front); the
+    // accumulators start at the bias (this lane's unit column), as addmm's beta * bias + x W^T does
+    auto prod3 = [&](const float (*tile)[T_HP], const f32x4 (&wt)[3][4], const float (&bias)[3],
+                     f32x4 (&out)[2][3]) {
       f32x4 av[2][4];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_tile_kernel(Dims d, Rep rp, co
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
 #pragma unroll
-        for (int gt = 0; gt < 3; ++gt) out[mt][gt] = f32x4{0, 0, 0, 0};
+        for (int gt = 0; gt < 3; ++gt) out[mt][gt] = f32x4{bias[gt], bias[gt], bias[gt], bias[gt]};
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -162,16 +162,16 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_tile_kernel(Dims d, Rep rp, co
     lds_barrier();   // #1: tables, h_{-1}; X1 tiles being built by the projection waves
     lds_barrier();   // #2: X1 of steps 0 and 1
     f32x4 gi[2][3];
-    prod3(S.x1[0], wih, gi);   // GI_0 (biases added in the gate math)
+    prod3(S.x1[0], wih, bi, gi);   // GI_0 = X1_0 W_ih^T + b_ih
     lds_barrier();   // #3
     float hprev[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     const auto hsb = buf_rsrc(w.Hs);
     // one step: the input gates of step t in gi_t (registers), those of step t + 1 into gi_n. The loop runs two steps
     // per iteration with the two sets swapping roles, so no register copy carries GI across the back edge.
     auto step = [&](int t, const f32x4 (&gi_t)[2][3], f32x4 (&gi_n)[2][3]) {
-      // GH_t = h_{t-1} W_hh^T
+      // GH_t = h_{t-1} W_hh^T + b_hh
       f32x4 gh[2][3];
-      prod3(S.hb[(t + 1) & 1], whh, gh);
+      prod3(S.hb[(t + 1) & 1], whh, bh, gh);
       // gates -> h_t (ATen gru_cell order: r, z from (W_h h + b_h) + gi; n = tanh(gi_n + r (W_hn h + b_hn));
       // h = (h_{t-1} - n) z + n)
       const auto gb = buf_rsrc(w.Gates + (int64_t)t * (4 * RH));
@@ -180,10 +180,10 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_tile_kernel(Dims d, Rep rp, co
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = 16 * mt + 4 * g + e, r = r0 + i;
-          const float rg = sigm_fast((gh[mt][0][e] + bhr) + (gi_t[mt][0][e] + bir));
-          const float zg = sigm_fast((gh[mt][1][e] + bhz) + (gi_t[mt][1][e] + biz));
-          const float ghn = gh[mt][2][e] + bhn;
-          const float ng = tanh_fast((gi_t[mt][2][e] + bin) + ghn * rg);
+          const float rg = sigm_fast(gh[mt][0][e] + gi_t[mt][0][e]);
+          const float zg = sigm_fast(gh[mt][1][e] + gi_t[mt][1][e]);
+          const float ghn = gh[mt][2][e];
+          const float ng = tanh_fast(gi_t[mt][2][e] + ghn * rg);
           const float h1 = (hprev[mt][e] - ng) * zg + ng;
           hprev[mt][e] = h1;
           S.hb[t & 1][i][j] = h1;
@@ -191,8 +191,8 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_tile_kernel(Dims d, Rep rp, co
           buf_st(hsb, st ? (((uint32_t)t * R + r) * H + j) * 4 : kDrop, h1);
           buf_st4(gb, st ? ((uint32_t)r * H + j) * 16 : kDrop, f32x4{rg, zg, ng, ghn});
         }
-      // GI of step t + 1 (X1_{t+1}, built by the projection waves in step t - 1)
-      prod3(S.x1[(t + 1) & 1], wih, gi_n);
+      // GI of step t + 1 = X1_{t+1} W_ih^T + b_ih (X1_{t+1}: built by the projection waves in step t - 1)
+      prod3(S.x1[(t + 1) & 1], wih, bi, gi_n);
       lds_barrier();
     };
     f32x4 gi2[2][3];
