@@ -428,6 +428,11 @@ def coma_bench(a):
         dist.destroy_process_group()
         return
     cpu = None if (a.no_cpu_baseline or world > 1) else coma_cpu_baseline(a.config, data)
+    # PMC bytes of the whole persistent chain launch, per critic step like `achieved` and `launch_ms`
+    traffic, traffic_src = (pmc_traffic(a.config, "coma_chain") if learner.critic_path() == "chain"
+                            else (None, "PMC covers the persistent chain only"))
+    if traffic is not None:
+        traffic, traffic_src = traffic / T, traffic_src + f"; the chain launch's bytes / T = {T} critic steps"
     line = {
         "metric": METRIC, "value": value, "unit": "samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
@@ -443,7 +448,8 @@ def coma_bench(a):
                                                  else "critic step chain (l1 + head + wgrad, x T)"),
                      "critic_path": learner.critic_path(),
                      "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "launch_ms": chain_ms / T,
+                     "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
+                     "launch_ms": chain_ms / T,
                      "flops_per_launch": step_flops,
                      "phases_ms": {k: float(np.mean([c[k] for c in chains])) for k in chains[0]}},
         "cpu_baseline": cpu,
