@@ -95,6 +95,9 @@ typedef int (*mc_allreduce_fn)(float* buf, int64_t count, void* stream, void* ct
 int mc_comm_attach(mc_handle* h, const uint8_t* id, int32_t rank, int32_t world);
 /* The same over a communicator the caller owns (see mq_comm_use): borrowed, never freed by the handle. */
 int mc_comm_use(mc_handle* h, void* nccl_comm);
+/* Drop the attached communicator (freed only if mc_comm_attach created it) and, if it carried the exchange steps,
+ * switch data parallelism off. A host that frees a communicator it lent with mc_comm_use detaches first. */
+int mc_comm_detach(mc_handle* h);
 int mc_set_data_parallel(mc_handle* h, mc_allreduce_fn allreduce, void* ctx, int32_t rank, float* scratch,
                          int64_t scratch_count);
 /* Replicated-critic data parallelism, for batches whose critic fits the persistent chain (B * n_agents <= 80, as

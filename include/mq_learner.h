@@ -92,8 +92,7 @@ int mq_bind(mq_handle* h, float* online, float* target, float* grad, float* sq_a
 int mq_forward_backward(mq_handle* h, const mq_replay* batch, void* stream);
 /* Normalise by sum(m), clip_grad_norm_(grad_norm_clip), RMSprop(lr, alpha, eps) step, write stats. */
 int mq_apply(mq_handle* h, void* stream);
-/* mq_forward_backward + mq_apply in one call. With MQ_FUSED_APPLY=1 in the environment at mq_create and no data
- * parallelism, the reduction's last pass and the optimiser step run as one launch (bitwise the two calls'). */
+/* mq_forward_backward + mq_apply in one call (with a communicator attached, the all-reduce between them too). */
 int mq_train_step(mq_handle* h, const mq_replay* batch, void* stream);
 /* Declare that the caller sums the gradient buffer across ranks between mq_forward_backward and mq_apply
  * (mq_apply then recomputes the global gradient norm from the reduced buffer). */
@@ -143,8 +142,7 @@ int mq_qmix_forward(const float* mixer, int32_t n_agents, int32_t state_dim, int
 
 /* Which kernel variants the last mq_forward_backward launched (test / profiling introspection; no device sync).
  * rw_fwd / rw_bwd: rows per workgroup of the unfused recurrences (0 when the fused kernel ran). */
-/* MQ_HYP_MIX: hypernet and mixer in one launch (hymix_kernel); mix then names the mixer instantiation */
-enum { MQ_HYP_NONE = 0, MQ_HYP_WS = 1, MQ_HYP_LDS = 2, MQ_HYP_GEMM = 3, MQ_HYP_MIX = 4 };
+enum { MQ_HYP_NONE = 0, MQ_HYP_WS = 1, MQ_HYP_LDS = 2, MQ_HYP_GEMM = 3 };
 enum { MQ_MIX_FAST16 = 0, MQ_MIX_FAST32 = 1, MQ_MIX_GENERIC = 2 };
 typedef struct mq_plan {
   int32_t rows;          /* R = batch_size * n_agents */

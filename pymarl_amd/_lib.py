@@ -32,7 +32,7 @@ EXPORTS = [
     "mc_copy_intermediate", "mc_set_timing", "mc_phase_times", "mc_last_critic_path", "mq_comm_unique_id", "mq_comm_attach",
     "mq_comm_world", "mq_comm_detach", "mc_comm_attach", "mc_set_data_parallel", "mc_critic_forward",
     "mc_critic_forward_workspace", "mc_set_actor_shard", "mq_comm_use", "mq_comm_create", "mq_comm_free",
-    "mc_comm_use",
+    "mc_comm_use", "mc_comm_detach",
 ]
 
 # mc_allreduce_fn (include/mc_coma.h): int (*)(float* buf, int64_t count, void* stream, void* ctx)
@@ -85,7 +85,7 @@ class MQPlan(ctypes.Structure):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
 
 
-HYP_NAMES = {0: "none", 1: "ws", 2: "lds", 3: "gemm", 4: "ws_mix"}
+HYP_NAMES = {0: "none", 1: "ws", 2: "lds", 3: "gemm"}
 MIX_NAMES = {0: "fast16", 1: "fast32", 2: "generic"}
 
 INLINE_IDS = 256   # MQ_INLINE_IDS: batches up to this size pass their episode ids in the kernel arguments
@@ -155,6 +155,7 @@ def load(required=True):
         "mq_comm_create": ([vp, i32, i32, ctypes.POINTER(vp)], ctypes.c_int),
         "mq_comm_free": ([vp], ctypes.c_int),
         "mc_comm_use": ([vp, vp], ctypes.c_int),
+        "mc_comm_detach": ([vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

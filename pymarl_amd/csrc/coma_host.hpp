@@ -638,6 +638,15 @@ int mc_comm_use(mc_handle* h, void* comm) {
   return mc_set_data_parallel(h, mc_rccl_allreduce, h, rank, h->comm_scratch, n);
 }
 
+int mc_comm_detach(mc_handle* h) {
+  if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
+  if (h->comm && h->comm_owned) (void)ncclCommDestroy(h->comm);
+  const bool was_rccl = h->dp_fn == mc_rccl_allreduce;
+  h->comm = nullptr;
+  h->comm_owned = false;
+  return was_rccl ? mc_set_data_parallel(h, nullptr, nullptr, 0, nullptr, 0) : MQ_OK;
+}
+
 int mc_set_timing(mc_handle* h, int32_t on) {
   if (!h) return set_err(MQ_ERR_ARG, "NULL handle");
   for (auto& e : h->ev)

@@ -20,9 +20,8 @@
 // B-fragments (W_hh, W_ih, W1's obs part, W2) stay in VGPRs for the whole T loop; the one-hot columns of W1 are
 // gathered from LDS. v_mfma_f32_16x16x4_f32 throughout (fp32 in, fp32 accumulate: the reference's arithmetic).
 //
-// Backward, gru_bwd_tile_kernel (online net): one workgroup = 16 rows, 256 threads, wave w again owns units
-// 16w .. 16w + 15 (gru_bwd_split_kernel: the same step on 512 threads, chain and weight-gradient roles). Per step t
-// (descending), two LDS barriers:
+// Backward, gru_bwd_split_kernel (online net): one workgroup = 16 rows, 512 threads in two roles (chain and
+// weight-gradient waves); waves w and w + 4 own units 16 (w & 3) .. + 15. Per step t (descending), two LDS barriers:
 //   dh = carry + dchosen W2[a_t];  dgi, dgh from the stored gates (lane-local, as the forward's gate math)
 //   carry_{t-1} = dh z + dgh W_hh         [16 x 192] x [192 x 64]
 //   dX1 = (dgi W_ih) o [X1 > 0]           [16 x 192] x [192 x 64]
@@ -58,8 +57,10 @@ inline int tile_kq1(int O) {
 constexpr int T_TMAX = 512;   // steps (t_len) the forward's per-step one-hot table holds
 constexpr int T_NOH = 80;     // one-hot columns (last action + agent id) of W1 staged in LDS
 inline bool tiles_ok(int I, int O, int A, int n, int Tp, int64_t RT) {
+  // RT * H * 4 bytes: the Hs stores go through one buffer descriptor (num_records 0x7FFFFFF0) with byte offsets up
+  // to RT * H * 4, so a larger batch would have its stores past 2 GiB dropped by the range check
   return tile_kq1(O) > 0 && A <= 48 && I <= 16 * T_NI && I - O <= T_NOH && Tp <= T_TMAX && n * O < (1 << 24) &&
-         RT * G3 < (int64_t(1) << 31);
+         RT * G3 < (int64_t(1) << 31) && RT * H * 4 < int64_t(0x7FFFFFF0);
 }
 
 template <int KQ1>
@@ -395,332 +396,15 @@ struct alignas(16) BwdTileLds {
   int agent[TR_B];
 };
 
-// grid = ceil(R / 16), 256 threads. slab_len / slab1_len: per-workgroup slab strides (len_rnn, H * I + H).
-template <int KQ1>
-__global__ __launch_bounds__(256, 1) void gru_bwd_tile_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
-                                                              Work w, int64_t slab_len, int64_t slab1_len) {
-  __shared__ BwdTileLds<KQ1> S;
-  constexpr int NS = (4 * KQ1 + 63) / 64;
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
-  const int ub = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int R = d.R, Tp = d.Tp, T = d.T, O = d.O, A = d.A, n = d.n, I = d.I;
-  const int NI = (I + 15) / 16;
-  const int r0 = blockIdx.x * TR_B;
-  const int j = 16 * ub + c;
-  const int nO = n * O;
-  const uint32_t RH = (uint32_t)R * H;
-
-  // ---- weights as B fragments: W[48 g + s][j] (K = the 192 gate columns, contiguous quarter per lane group)
-  float whh[48], wih[48];
-  {
-    const float* Wh = P + L.o[MQ_P_RNN_W_HH];
-    const float* Wi = P + L.o[MQ_P_RNN_W_IH];
-#pragma unroll
-    for (int s = 0; s < 48; ++s) {
-      whh[s] = Wh[(int64_t)(48 * g + s) * H + j];
-      wih[s] = Wi[(int64_t)(48 * g + s) * H + j];
-    }
-  }
-  for (int e = tid; e < 48 * H; e += 256) (&S.w2[0][0])[e] = e < A * H ? P[L.o[MQ_P_FC2_W] + e] : 0.0f;
-  for (int e = tid; e < 3 * TR_B * T_HP; e += 256) (&S.hb[0][0][0])[e] = 0.0f;
-  for (int e = tid; e < 2 * TR_B * (16 * T_NI + 4); e += 256) (&S.xin[0][0][0])[e] = 0.0f;
-  if (tid < TR_B) {
-    const int r = min(r0 + tid, R - 1);
-    S.agent[tid] = r - (int)fdiv((uint32_t)r, d.dN) * n;
-  }
-
-  // ---- per-row replay addressing: obs rows 4 ub + i (wave-uniform bases); lane tid < 16: row tid's action,
-  // filled and dchosen streams (staged into LDS per step)
-  auto row_of = [&](int i) { return min(r0 + i, R - 1); };
-  const float* rowb[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = row_of(4 * ub + i);
-    const int b = (int)fdiv((uint32_t)r, d.dN), ag = r - b * n;
-    rowb[i] = rp.obs + (rp.ep(b) * d.t_stride * n + ag) * (int64_t)O;
-  }
-  const int rl = row_of(tid & 15);
-  const bool rl_live = r0 + (tid & 15) < R;
-  const int bl = (int)fdiv((uint32_t)rl, d.dN);
-  const int64_t* act_l = rp.actions + rp.ep(bl) * d.t_stride * n + (rl - bl * n);
-  const int64_t* fil_l = rp.filled + rp.ep(bl) * d.t_stride;
-
-  // ---- the prefetched inputs of one step: own (row, unit) pairs; the obs rows go straight to LDS (glds)
-  struct In {
-    float gr[4], gz[4], gn[4], ghn[4];   // gates r, z, n and W_hn h + b_hn
-    float hp[4], x1[4];                  // h_{t-1}, X1_t
-  };
-  // tid < 16: the raw dchosen, a_t, filled[t-1] and a_{t-1} words of row tid for the step two ahead (the selects
-  // wait for store_row, so no load result is consumed in the step that issues it)
-  float dch_n = 0.0f;
-  int act_n = 0, fil_n = 0, apv_n = 0, t_n = 0;
-  auto fetch = [&](int t, In& x) {
-    const int tc = max(t, 0), tm = max(t - 1, 0);
-    const f32x4* gbase = (const f32x4*)(w.Gates + (int64_t)tc * (4 * RH));
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int r = row_of(4 * g + e);
-      const f32x4 gv = gbase[(uint32_t)r * H + j];   // the tile path's [RT][H][4] gate record
-      x.gr[e] = gv[0];
-      x.gz[e] = gv[1];
-      x.gn[e] = gv[2];
-      x.ghn[e] = gv[3];
-      x.hp[e] = ld_u32(w.Hs + (int64_t)tm * RH, (uint32_t)r * H + j);
-      x.x1[e] = ld_u32(w.X1 + (int64_t)tc * RH, (uint32_t)r * H + j);
-    }
-    // obs rows of step tc straight into xin[tc & 1] (LDS-DMA, lane-linear: columns 64 s + lane; columns past O
-    // read a clamped in-row address and are overwritten by the one-hot pass before anyone reads them)
-    float(*xi)[16 * T_NI + 4] = S.xin[tc & 1];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-        __builtin_amdgcn_global_load_lds(rowb[i] + (int64_t)tc * nO + min(lane + 64 * s, O - 1),
-                                         (__attribute__((address_space(3))) void*)&xi[4 * ub + i][64 * s], 4, 0, 0);
-  };
-  // row tid's dchosen and a_t of step t, and a_{t-1} (when t > 0 and slot t - 1 was filled: the last-action
-  // one-hot). Rows past R (a partial last tile) get dchosen = 0: their dh, gate derivatives and every gradient
-  // contribution are then exactly 0; step T has no dchosen (q_learner.py:55 uses mac_out[:, :-1]).
-  auto fetch_row = [&](int t) {
-    const int tc = min(max(t, 0), Tp - 1), tp = max(tc - 1, 0);
-    dch_n = ld_u32(w.dch + (int64_t)min(tc, T - 1) * R, (uint32_t)rl);
-    act_n = *(const int*)(act_l + (int64_t)tc * n);
-    fil_n = *(const int*)(fil_l + tp);
-    apv_n = *(const int*)(act_l + (int64_t)tp * n);
-    t_n = t;
-  };
-  auto store_row = [&](int t) {   // into the ring slot of step t (read during step t: two barriers later)
-    const bool live = t_n >= 0 && t_n < Tp;
-    S.dchs[t & 3][tid] = (rl_live && live && t_n < T) ? dch_n : 0.0f;
-    S.acts[t & 3][tid] = act_n;
-    S.ap[t & 3][tid] = (d.last_action && live && t_n > 0 && fil_n) ? apv_n : -1;
-  };
-  // stage step t's tiles: h_{t-1} -> hb[(t - 1) % 3], X1_t -> x1, the one-hot columns of xin[t & 1] (its obs
-  // columns arrived by LDS-DMA), dchosen / a_t -> the row arrays
-  auto stage = [&](int t, const In& x) {
-    drain_vmem();   // this wave's loads, including its LDS-DMA rows, have landed
-    const int hbuf = (t + 2) % 3;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int i = 4 * g + e;
-      S.hb[hbuf][i][j] = t > 0 ? x.hp[e] : 0.0f;
-      S.x1[i][j] = x.x1[e];
-    }
-    float(*xi)[16 * T_NI + 4] = S.xin[t & 1];
-    // one-hot columns [O, 16 NI) of rows 4 ub .. 4 ub + 3 (this wave's LDS-DMA rows), zeros and ones in one pass
-    const int wd = 16 * NI - O;
-    const int* apt = S.ap[t & 3];
-    for (int e = lane; e < 4 * wd; e += 64) {
-      const int i = 4 * ub + e / wd, col = e % wd;
-      const bool one = (d.last_action && col < A && col == apt[i]) ||
-                       (d.agent_id && col == (d.last_action ? A : 0) + S.agent[i]);
-      xi[i][O + col] = one ? 1.0f : 0.0f;
-    }
-  };
-
-  f32x4 acc_hh[3][4], acc_ih[3][4], acc_w1[T_NI], acc_w2[3];
-#pragma unroll
-  for (int m = 0; m < 3; ++m)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) { acc_hh[m][q] = f32x4{0, 0, 0, 0}; acc_ih[m][q] = f32x4{0, 0, 0, 0}; }
-#pragma unroll
-  for (int q = 0; q < T_NI; ++q) acc_w1[q] = f32x4{0, 0, 0, 0};
-#pragma unroll
-  for (int m = 0; m < 3; ++m) acc_w2[m] = f32x4{0, 0, 0, 0};
-  float dbi[3] = {0, 0, 0}, dbh[3] = {0, 0, 0}, db1 = 0.0f, db2[3] = {0, 0, 0};
-  float carry[4] = {0, 0, 0, 0};
-
-  // ---- prologue: a_{t-1} of the two top steps into the ring, step Tp - 1's inputs in registers
-  In cur;
-  if (tid < TR_B) {
-    fetch_row(Tp - 1);
-    store_row(Tp - 1);
-  }
-  lds_barrier();   // the zeroed xin / hb and the ring before any LDS-DMA or stage writes
-  if (tid < TR_B) fetch_row(Tp - 2);   // stored by the first iteration
-  fetch(Tp - 1, cur);
-
-  for (int t = Tp - 1; t >= 0; --t) {
-    // P0: stage step t (its loads were issued during step t + 1)
-    stage(t, cur);
-    if (tid < TR_B) store_row(t - 1);   // fetched during step t + 1
-    // P1: dh and the gate derivatives of this lane's own (row, unit) pairs
-    float dh[4], zz[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int i = 4 * g + e;
-      const float dchv = S.dchs[t & 3][i];
-      const int a = min(max(S.acts[t & 3][i], 0), A - 1);
-      dh[e] = carry[e] + dchv * S.w2[a][j];
-      const float gr = cur.gr[e], gz = cur.gz[e], gn = cur.gn[e], ghn = cur.ghn[e];
-      const float hp = t > 0 ? cur.hp[e] : 0.0f;
-      const float dn = dh[e] * (1.0f - gz);
-      const float dz = dh[e] * (hp - gn);
-      const float dan = dn * (1.0f - gn * gn);
-      const float dar = (dan * ghn) * (gr * (1.0f - gr));
-      const float daz = dz * (gz * (1.0f - gz));
-      S.dgi[i][j] = dar; S.dgi[i][H + j] = daz; S.dgi[i][2 * H + j] = dan;
-      S.dgh[i][j] = dar; S.dgh[i][H + j] = daz; S.dgh[i][2 * H + j] = dan * gr;
-      dbi[0] += dar; dbi[1] += daz; dbi[2] += dan;
-      dbh[0] += dar; dbh[1] += daz; dbh[2] += dan * gr;
-      zz[e] = gz;
-    }
-    lds_barrier();   // B1: dgi / dgh, h_{t-1}, X1, xin of step t
-    // P2: the next step's loads, in flight under this step's MFMAs
-    if (t > 0) fetch(t - 1, cur);
-    if (tid < TR_B) fetch_row(t - 2);
-    // P3: carry_{t-1} = dh z + dgh W_hh;  dX1 = (dgi W_ih) o [X1 > 0]
-    {
-      f32x4 ca = {0, 0, 0, 0}, cb = {0, 0, 0, 0};
-      const float* ah = &S.dgh[c][48 * g];
-#pragma unroll
-      for (int q = 0; q < 12; ++q) {
-        const f32x4 vh = *(const f32x4*)(ah + 4 * q);
-        ca = mfma16x4(vh[0], whh[4 * q], ca);
-        cb = mfma16x4(vh[1], whh[4 * q + 1], cb);
-        ca = mfma16x4(vh[2], whh[4 * q + 2], ca);
-        cb = mfma16x4(vh[3], whh[4 * q + 3], cb);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) carry[e] = dh[e] * zz[e] + (ca[e] + cb[e]);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    {
-      f32x4 xa = {0, 0, 0, 0}, xb = {0, 0, 0, 0};
-      const float* ai = &S.dgi[c][48 * g];
-#pragma unroll
-      for (int q = 0; q < 12; ++q) {
-        const f32x4 vi = *(const f32x4*)(ai + 4 * q);
-        xa = mfma16x4(vi[0], wih[4 * q], xa);
-        xb = mfma16x4(vi[1], wih[4 * q + 1], xb);
-        xa = mfma16x4(vi[2], wih[4 * q + 2], xa);
-        xb = mfma16x4(vi[3], wih[4 * q + 3], xb);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = S.x1[4 * g + e][j] > 0.0f ? xa[e] + xb[e] : 0.0f;   // relu'(X1_t)
-        S.dx1[4 * g + e][j] = v;
-        db1 += v;
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // dW_hh += dgh^T h_{t-1}, dW_ih += dgi^T X1 (K = the 16 rows, k = 4 g + s)
-    {
-      const int hbuf = (t + 2) % 3;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int row = 4 * g + s;
-        float a_h[3], a_i[3], b_h[4], b_x[4];
-#pragma unroll
-        for (int m = 0; m < 3; ++m) {
-          a_h[m] = S.dgh[row][16 * (4 * m + ub) + c];
-          a_i[m] = S.dgi[row][16 * (4 * m + ub) + c];
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          b_h[q] = S.hb[hbuf][row][16 * q + c];
-          b_x[q] = S.x1[row][16 * q + c];
-        }
-#pragma unroll
-        for (int m = 0; m < 3; ++m)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            acc_hh[m][q] = mfma16x4(a_h[m], b_h[q], acc_hh[m][q]);
-            acc_ih[m][q] = mfma16x4(a_i[m], b_x[q], acc_ih[m][q]);
-          }
-      }
-    }
-    lds_barrier();   // B2: dX1 of step t
-    // P4: dW1 += dX1^T xin_t;  dW2 += onehot(a_t)^T (dchosen h_t);  db2
-    {
-      const float(*xi)[16 * T_NI + 4] = S.xin[t & 1];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int row = 4 * g + s;
-        const float av = S.dx1[row][j];
-#pragma unroll
-        for (int q = 0; q < T_NI; ++q)
-          if (q < NI) acc_w1[q] = mfma16x4(av, xi[row][16 * q + c], acc_w1[q]);
-      }
-      const int hbuf = t % 3;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int row = 4 * g + s;
-        const float dchv = S.dchs[t & 3][row];
-        const int aw = S.acts[t & 3][row];
-        const float bv = S.hb[hbuf][row][j];
-#pragma unroll
-        for (int m = 0; m < 3; ++m) {
-          const float av = aw == 16 * m + c ? dchv : 0.0f;
-          acc_w2[m] = mfma16x4(av, bv, acc_w2[m]);
-          if (ub == 0) db2[m] += av;   // rows 4 g + s of this lane group; the groups are summed at the end
-        }
-      }
-    }
-  }
-
-  // ---- slabs: [w_ih | w_hh | b_ih | b_hh | fc2.w | fc2.b] and [fc1.w | fc1.b], parameter layout
-  const int64_t base = L.o[MQ_P_RNN_W_IH];
-  float* slab = w.slab_rnn + (int64_t)blockIdx.x * slab_len;
-  float* slab1 = w.slab_fc1 + (int64_t)blockIdx.x * slab1_len;
-  const int64_t o_hh = L.o[MQ_P_RNN_W_HH] - base, o_bi = L.o[MQ_P_RNN_B_IH] - base,
-                o_bh = L.o[MQ_P_RNN_B_HH] - base, o_w2 = L.o[MQ_P_FC2_W] - base, o_b2 = L.o[MQ_P_FC2_B] - base;
-#pragma unroll
-  for (int m = 0; m < 3; ++m)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int gc = 16 * (4 * m + ub) + 4 * g + e, u = 16 * q + c;
-        slab[gc * H + u] = acc_ih[m][q][e];
-        slab[o_hh + gc * H + u] = acc_hh[m][q][e];
-      }
-#pragma unroll
-  for (int q = 0; q < T_NI; ++q)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int u = 16 * ub + 4 * g + e, col = 16 * q + c;
-      if (q < NI && col < I) slab1[(int64_t)u * I + col] = acc_w1[q][e];
-    }
-#pragma unroll
-  for (int m = 0; m < 3; ++m)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int a = 16 * m + 4 * g + e;
-      if (a < A) slab[o_w2 + a * H + j] = acc_w2[m][e];
-    }
-  // bias gradients: this lane's partials cover rows 4 g .. 4 g + 3 (db2 too); sum the four lane groups
-  auto gsum = [](float v) {
-    v += __shfl_xor(v, 16, 64);
-    return v + __shfl_xor(v, 32, 64);
-  };
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const float si = gsum(dbi[k]), sh = gsum(dbh[k]);
-    if (g == 0) { slab[o_bi + k * H + j] = si; slab[o_bh + k * H + j] = sh; }
-  }
-  {
-    const float s1 = gsum(db1);
-    if (g == 0) slab1[(int64_t)H * I + j] = s1;
-  }
-  if (ub == 0) {
-#pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const float s2 = gsum(db2[m]);
-      if (g == 0 && 16 * m + c < A) slab[o_b2 + 16 * m + c] = s2;
-    }
-  }
-}
-
 // grid = ceil(R / 16), 512 threads. slab_len / slab1_len: per-workgroup slab strides (len_rnn, H * I + H).
-// The same step as gru_bwd_tile_kernel on two waves per SIMD with split roles, both on units 16 ub .. 16 ub + 15
-// (ub = wave & 3), two barriers a step:
+// Two waves per SIMD with split roles, both on units 16 ub .. 16 ub + 15 (ub = wave & 3), two barriers a step:
 //   chain waves 0-3:   stage, dh and the gate derivatives | B1 | carry              | B2 | dW1 column tiles [0, 12)
 //   weight waves 4-7:                                      | B1 | dX1, dW_hh, dW_ih | B2 | dW1 tiles [12, NI), dW2
 // (96 / 196 MFMAs a step at cfg3's shape). The serial chain's LDS and MFMA latencies are filled by the weight
 // waves' work on the same SIMD, and each role holds only its own weights, accumulators and prefetches (the chain:
 // W_hh and the next step's gate / h / X1 / obs loads; the weight waves: W_ih and 100 accumulators), which is what
-// fits two roles in 2 x 256 registers. Same per-output MFMA order as gru_bwd_tile_kernel.
+// fits two roles in 2 x 256 registers (one role per wave needed 480 registers in one wave per SIMD: 1.99 ms
+// against 1.27 ms at cfg3; that variant was removed in round 5).
 constexpr int T_NIC = 12;               // dW1 column tiles of the chain waves
 constexpr int T_NIW = T_NI - T_NIC;     // of the weight waves
 template <int KQ1>

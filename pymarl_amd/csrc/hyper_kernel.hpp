@@ -307,125 +307,4 @@ __global__ __launch_bounds__(HYWS_THREADS) void hyper_ws_kernel(Dims d, Rep rp, 
   if (stamp) stm[9] = __builtin_amdgcn_s_memtime();
 }
 
-// ---- The QMIX hypernet and the mixer in one launch (hymix_kernel): the HYP rows never leave the CU.
-// A workgroup owns HMX_R = 16 mixer rows m = t B + b, both nets: waves 0-3 compute the online hypernet on
-// state_t, waves 4-7 the target's on state_{t+1}, each wave the N-tiles wl, wl + 4, .. of its net's NH outputs
-// (16 columns each; E % 16 == 0 keeps a tile inside one of hyper_w_1 / hyper_w_final / hyper_b_1 / V.0). The state
-// rows are the A operand held in registers for all of the wave's tiles; the weight rows stream from L2 straight into
-// registers (the next tile's loads in flight under the current tile's 48 MFMAs), so the phase has no LDS staging
-// and no barrier. The MFMA sequence per tile (K = 192 in lane-group quarters, k = 48 g + 4 mm + e, one accumulator)
-// and the bias add are hyper_ws_kernel's, so HYP is bitwise hyper_ws_kernel's, and S0 (the dW_hyper operand) is
-// written from the same registers. Then every wave runs mix_fast_row on two of the rows with its HYP rows read from
-// LDS, and the loss / V.2 partials are summed per 4 consecutive rows in mix_fast_kernel's order: the outputs (dHYP,
-// dchosen, loss_part, slab_v2, double-Q actions) are bitwise the two-kernel path's.
-constexpr int HMX_R = 16;
-constexpr int HMX_NHP = 452;   // LDS pitch of a HYP row: NH <= 448
-template <int MN>
-struct alignas(16) HymixLds {
-  float hyp[2][HMX_R][HMX_NHP];
-  MixScratch<MN> sc[8];
-  float red[HMX_R][8];
-  float v2red[HMX_R][65];
-};
-inline bool hymix_ok(int S, int E, int NH, int n, int A, int64_t M) {
-  return hyper_ws_ok(S, E, NH, M) && NH <= HMX_NHP - 4 && n <= 16 && A <= 32 && E <= 64;
-}
-
-template <int MA, int MN>
-__global__ __launch_bounds__(512) void hymix_kernel(Dims d, Rep rp, const float* __restrict__ P0,
-                                                    const float* __restrict__ P1, Lay L, Work w,
-                                                    int32_t* curmax_out) {
-  __shared__ HymixLds<MN> S;
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c16 = lane & 15;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int z = wv >> 2, wl = wv & 3;
-  const int m0 = blockIdx.x * HMX_R;
-  const int Sd = d.S, n = d.n, E = d.E, NT = d.NH / 16;
-  const float* __restrict__ P = z ? P1 : P0;
-  {
-    // ---- A operand: state row m0 + c16 at t + z, this lane group's K quarter [48 g, 48 g + 48), zero past S / M
-    f32x4 av[12];
-    {
-      const int m = m0 + c16, mc = min(m, d.M - 1);
-      const int t = (int)fdiv((uint32_t)mc, d.dB), b = mc - t * d.B;
-      const float* row = rp.state + (rp.ep(b) * d.t_stride + t + z) * (int64_t)Sd;
-#pragma unroll
-      for (int q = 0; q < 12; ++q) {
-        const int k = 48 * g + 4 * q;
-        av[q] = (k < Sd && m < d.M) ? *(const f32x4*)(row + k) : f32x4{0, 0, 0, 0};
-      }
-      if (wv == 0 && m < d.M && w.S0) {   // the gathered online rows for dW_hyper
-#pragma unroll
-        for (int q = 0; q < 12; ++q)
-          if (48 * g + 4 * q < Sd) *(f32x4*)(w.S0 + (int64_t)m * Sd + 48 * g + 4 * q) = av[q];
-      }
-    }
-    // ---- B operand: weight rows j0 + c16 of the tile's segment, K quarter g: each lane's 48 K values are contiguous,
-    // 12 dwordx4 buffer loads through the parameter descriptor (past the buffer: 0; past S within a row: the next
-    // row's finite values, times the zero A padding) plus the bias; two register sets with compile-time names (the
-    // tile loop is unrolled by two), so the next tile's loads are in flight under the current tile's 48 MFMAs
-    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)P, (short)0, (int)(L.o[MQ_P_COUNT] * sizeof(float)), 0x00020000);
-    f32x4 bwa[12], bwb[12];
-    float bja = 0.0f, bjb = 0.0f;
-    auto fetch = [&](int nt, f32x4 (&dst)[12], float& bj) {
-      const HypSeg sg = hyp_seg(L, n * E, E, 16 * nt);
-      const int base = (int)((sg.w + (int64_t)(sg.row + c16) * Sd + 48 * g) * 4);
-#pragma unroll
-      for (int q = 0; q < 12; ++q)
-        dst[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, base + 16 * q, 0, 0));
-      bj = P[sg.b + sg.row + c16];
-    };
-    auto tile = [&](int nt, const f32x4 (&bw)[12], float bj) {
-      f32x4 acc = {0, 0, 0, 0};
-#pragma unroll
-      for (int mm = 0; mm < 12; ++mm)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc = mfma16x4(av[mm][e], bw[mm][e], acc);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) S.hyp[z][4 * g + e][16 * nt + c16] = acc[e] + bj;
-    };
-#if defined(MQ_HYMIX_EXP) && MQ_HYMIX_EXP == 2   // diagnostic build: the mixer part alone (r04n)
-    int nt = NT;
-#else
-    int nt = wl;
-#endif
-    if (nt < NT) fetch(nt, bwa, bja);
-    for (; nt < NT; nt += 8) {
-      if (nt + 4 < NT) fetch(nt + 4, bwb, bjb);
-      tile(nt, bwa, bja);
-      if (nt + 4 >= NT) break;
-      if (nt + 8 < NT) fetch(nt + 8, bwa, bja);
-      tile(nt + 4, bwb, bjb);
-    }
-  }
-  __syncthreads();
-  // ---- the mixer: wave wv takes rows 2 wv and 2 wv + 1 of the block
-#if defined(MQ_HYMIX_EXP) && MQ_HYMIX_EXP == 1
-  if (d.M < 0)
-#endif
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int sl = 2 * wv + k;
-    mix_fast_row<MA, MN>(d, rp, P0, P1, L, w, curmax_out, m0 + sl, lane, &S.hyp[0][sl][0], &S.hyp[1][sl][0],
-                         S.sc[wv], S.red[sl], S.v2red[sl]);
-  }
-  __syncthreads();
-  // per 4 consecutive rows (mix_fast_kernel's blocks), in its order
-  const int nblk = (d.M + 3) / 4;
-  if (tid < 32) {
-    const int q = tid >> 3, c = tid & 7, blk = m0 / 4 + q;
-    if (blk < nblk)
-      w.loss_part[(int64_t)blk * 8 + c] =
-          c < 5 ? ((S.red[4 * q][c] + S.red[4 * q + 1][c]) + (S.red[4 * q + 2][c] + S.red[4 * q + 3][c])) : 0.0f;
-  }
-  for (int i = tid; i < 4 * (E + 1); i += 512) {
-    const int q = i / (E + 1), ee = i - q * (E + 1), blk = m0 / 4 + q;
-    const int e = ee == E ? 64 : ee;
-    if (blk < nblk)
-      w.slab_v2[(int64_t)blk * (E + 1) + ee] =
-          (S.v2red[4 * q][e] + S.v2red[4 * q + 1][e]) + (S.v2red[4 * q + 2][e] + S.v2red[4 * q + 3][e]);
-  }
-}
-
 }  // namespace mq

@@ -223,8 +223,8 @@ namespace mq {
 // The generic kernel fetches them in dependent stages (action -> chosen, argmax blocks -> target value, then the
 // hypernet rows after a barrier). Same arithmetic in the same order: bitwise-identical outputs.
 //
-// mix_fast_row is one wave's (t, b) row m: hon / htg point at its hypernet outputs (HYP rows in global memory for
-// mix_fast_kernel, LDS rows for hymix_kernel), `sc` is the wave's LDS scratch, and the row's loss / V.2 partials
+// mix_fast_row is one wave's (t, b) row m: hon / htg point at its hypernet outputs (HYP rows in global memory),
+// `sc` is the wave's LDS scratch, and the row's loss / V.2 partials
 // land in red_slot[0..4] / v2_slot[0..64] for the caller's fixed-order block sums. Two workgroup barriers inside:
 // every wave of the workgroup must call it the same number of times.
 template <int MN>

@@ -90,14 +90,13 @@ struct mq_handle {
   bool force_unfused_bwd = getenv("MQ_UNFUSED_BWD") != nullptr;   // A/B switch for the fused BPTT
   // rows up to which the fused BPTT (one row per workgroup, one workgroup per CU) is used: past the CU count the
   // rows run as a second wave of workgroups, which still beats gru_bwd<2> + dX1 + dW1 at configs[3]'s shard
-  // (R = 320); MQ_FUSED_BWD_RMAX=256 restores the round-2 cut-over for A/B runs
-  int fused_bwd_rmax = getenv("MQ_FUSED_BWD_RMAX") ? atoi(getenv("MQ_FUSED_BWD_RMAX")) : 512;
-  int dwh_split = getenv("MQ_DWH_SPLIT") ? atoi(getenv("MQ_DWH_SPLIT")) : 8;   // m-slices of the dW_hyper pass
+  // (R = 320; round 3)
+  static constexpr int fused_bwd_rmax = 512;
+  // m-slices of the dW_hyper pass (A/B at cfg2, DESIGN §3: 4 / 8 / 16 / 32 -> 238.5 / 235.1 / 236.3 / 237.4 us)
+  static constexpr int dwh_split = 8;
   // the row-tile MFMA forward / BPTT (gru_tiles.hpp) for batches past the one-row fused kernels (R > 512 rows);
   // MQ_ROW_TILES=1 forces it on any batch it can take (tests), =0 turns it off (A/B: the unfused GEMM path)
   int row_tiles = getenv("MQ_ROW_TILES") ? atoi(getenv("MQ_ROW_TILES")) : -1;
-  // MQ_HYMIX=1: the QMIX hypernet and mixer in one launch (hymix_kernel, bitwise the two-kernel path)
-  bool hymix = getenv("MQ_HYMIX") && atoi(getenv("MQ_HYMIX")) == 1;
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
   ncclComm_t comm = nullptr;   // mq_comm_attach / mq_comm_use: the library all-reduces the grad buffer itself
   int comm_world = 0;
@@ -504,22 +503,9 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     }
   }
   h->nblk_mix = (d.M + 3) / 4;
-  bool mixed = false;   // hymix_kernel ran the mixer too
   if (c.mixer == MQ_MIXER_QMIX && !hyp_in_fwd) {
     pt.begin(PH_HYP);
-    if (h->hymix && hymix_ok(d.S, d.E, d.NH, d.n, d.A, d.M)) {
-      plan.hyper = MQ_HYP_MIX;
-      plan.mix = d.A <= 16 ? MQ_MIX_FAST16 : MQ_MIX_FAST32;
-      const dim3 grid((d.M + HMX_R - 1) / HMX_R);
-      if (d.A <= 16)
-        hipLaunchKernelGGL((hymix_kernel<16, 16>), grid, dim3(512), 0, s, d, rp, (const float*)h->on,
-                           (const float*)h->tg, L, w, curmax);
-      else
-        hipLaunchKernelGGL((hymix_kernel<32, 16>), grid, dim3(512), 0, s, d, rp, (const float*)h->on,
-                           (const float*)h->tg, L, w, curmax);
-      MQ_HIP(hipGetLastError());
-      mixed = true;
-    } else if (hyper_ws_ok(d.S, d.E, d.NH, d.M)) {
+    if (hyper_ws_ok(d.S, d.E, d.NH, d.M)) {
       plan.hyper = MQ_HYP_WS;
       // wave-specialised weight streaming (hyper_kernel.hpp)
       hipLaunchKernelGGL(hyper_ws_kernel<0>, dim3((d.M + HYR - 1) / HYR, 2), dim3(HYWS_THREADS),
@@ -539,7 +525,7 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     }
   }
   pt.begin(PH_MIX);
-  if (!mixed) {
+  {
     const bool fast = d.n <= 16 && d.E <= 64;   // mix_kernel serves the rest (n > 16 or A > 32)
     plan.mix = fast && d.A <= 16 ? MQ_MIX_FAST16 : fast && d.A <= 32 ? MQ_MIX_FAST32 : MQ_MIX_GENERIC;
     if (fast && d.A <= 16)
@@ -563,13 +549,9 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     h->nsplit_fc1 = nblk;
     const int64_t l1 = (int64_t)mq::H * d.I + mq::H;
     const float* P0 = h->on;
-    // the two-role (chain / weight-gradient waves) BPTT, 512 threads; MQ_BWD_SPLIT=0: one wave per SIMD, 256 threads
-    const bool split = !(getenv("MQ_BWD_SPLIT") && atoi(getenv("MQ_BWD_SPLIT")) == 0);
-#define MQ_BWD_TILE(K)                                                                                          \
-  if (split)                                                                                                    \
-    hipLaunchKernelGGL(gru_bwd_split_kernel<K>, dim3(nblk), dim3(512), 0, s, d, rp, P0, L, w, h->len_rnn, l1); \
-  else                                                                                                          \
-    hipLaunchKernelGGL(gru_bwd_tile_kernel<K>, dim3(nblk), dim3(256), 0, s, d, rp, P0, L, w, h->len_rnn, l1);
+    // the two-role (chain / weight-gradient waves) BPTT, 512 threads
+#define MQ_BWD_TILE(K) \
+  hipLaunchKernelGGL(gru_bwd_split_kernel<K>, dim3(nblk), dim3(512), 0, s, d, rp, P0, L, w, h->len_rnn, l1);
     if (kq1 == 8) { MQ_BWD_TILE(8) }
     else if (kq1 == 20) { MQ_BWD_TILE(20) }
     else if (kq1 == 40) { MQ_BWD_TILE(40) }

@@ -17,7 +17,8 @@ every rank passes the SAME global sample to train() and trains its share of it, 
 * "exchange": every rank trains its shard, and the library sums the global per-step mask sums, each live critic
   step's gradient, the critic stat sums and the agent gradient across ranks (T + 3 all-reduces per train;
   include/mc_coma.h, mc_set_data_parallel).
-The ranks' agreement on the global sample is checked once (`args.learner_dp_check`, dp.check_same_batch): in
+The ranks' agreement on the global sample (ids and contents) is checked on a call-count schedule that is the same on
+every rank (`args.learner_dp_check`, dp.DPCheck / dp.check_same_batch): in
 "replicated" mode every rank's critic must see the same batch or the critics drift apart silently. A batch that is
 already a shard is rejected. Under an RCCL process group the exchanges run on the process's library communicator
 (dp.SharedComm: mq_comm_create once, mc_comm_use per handle), in stream order with no Python callback; other backends
@@ -38,7 +39,7 @@ from torch.optim import RMSprop
 from .. import _lib
 from ..modules.critics.coma import COMACritic
 from ..modules.flat import pack, rebind
-from .dp import SharedComm, dp_world, local_shard, native_comm_wanted, shard_bounds
+from .dp import DPCheck, SharedComm, dp_world, local_shard, native_comm_wanted, shard_bounds
 from .q_learner import replay_view
 from ..components.episode_buffer import is_replay_view
 
@@ -97,8 +98,7 @@ class COMALearner:
         self._handle_key = None
         self._steps = 0
         self.dp = bool(getattr(args, "learner_dp", False))
-        self.dp_check = getattr(args, "learner_dp_check", "first")   # "first" | "always" | "off" (see QLearner)
-        self._dp_checked = None
+        self.dp_check = DPCheck(getattr(args, "learner_dp_check", None))   # call-count schedule (see QLearner)
         self._dp_cb = None
         self._dp_scratch = None
 
@@ -135,6 +135,8 @@ class COMALearner:
     def _get_handle(self, batch):
         T = batch.source.max_seq_length if is_replay_view(batch) else batch.max_seq_length
         need_b = max(batch.batch_size, getattr(self.args, "batch_size", 1))
+        if self._handle is not None and self._handle.native and self._handle.comm_gen != SharedComm.generation:
+            self._handle = None   # its communicator was freed (SharedComm.free detached it): rebuild and re-attach
         if self._handle is None or self._handle_key[0] < need_b or self._handle_key[1] < T:
             cfg = make_coma_config(self.args, self.mac.agent.input_dim, need_b, T)
             h = _lib.ComaHandle(cfg)
@@ -148,8 +150,7 @@ class COMALearner:
             if self._dp_active():
                 rank, world = dp_world()
                 if native_comm_wanted(self._critic.device):
-                    _lib.check(h.lib.mc_comm_use(h.h, SharedComm.get(h.lib, self._critic.device)))
-                    h.native = True
+                    SharedComm.lend(h, "mc_comm_use", "mc_comm_detach", self._critic.device)
                 else:
                     self._dp_scratch = th.zeros(8 * T, dtype=th.float32, device=self._critic.device)
                     self._dp_cb = _lib.MC_ALLREDUCE_FN(self._allreduce)
@@ -200,11 +201,9 @@ class COMALearner:
         mode = self.dp_mode(batch.batch_size)
         if mode is not None:
             rank, world = dp_world()
-            key = (batch.batch_size, getattr(batch, "t_len", batch.max_seq_length), world)
-            check = self.dp_check == "always" or (self.dp_check != "off" and self._dp_checked != key)
+            check = self.dp_check.due()
             local = local_shard(batch, rank, world, check=check, device=self._critic.device)   # validates too
-            if check:
-                self._dp_checked = key
+            self.dp_check.done += int(check)
             if mode == "exchange":     # this rank's shard through every step, summed in the library
                 batch = local
         h = self._get_handle(batch)

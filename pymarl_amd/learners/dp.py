@@ -3,9 +3,10 @@
 Contract (the same for QLearner and COMALearner): every rank calls `learner.train(batch, ...)` with the SAME GLOBAL
 sample, exactly as the reference's run loop does (run.py:207-219: `buffer.sample(batch_size)`, `[:, :max_t]`,
 `.to(device)`). Ranks run with the same seed, so `ReplayBuffer.sample`'s `np.random.choice` draws the same episode
-ids on every rank. The learner keeps its own contiguous shard of the episodes (`local_shard`), checks once that the
-ranks really passed the same sample (`check_same_batch`: a fingerprint of the ids, batch size and t_len, compared with
-one MAX all-reduce), and rejects a batch that was already sharded (it would be sharded twice).
+ids on every rank. The learner keeps its own contiguous shard of the episodes (`local_shard`), checks on a call-count
+schedule that is the same on every rank (`DPCheck`) that the ranks really passed the same sample (`check_same_batch`: a
+fingerprint of the batch size, t_len, episode ids and a digest of the sampled rows' contents, compared with one MAX
+all-reduce), and rejects a batch that was already sharded (it would be sharded twice).
 
 Every rank backpropagates the UNNORMALISED loss sum (td*m)^2 of its shard; the gradient buffer carries the
 mask / stats sums in its tail (include/mq_learner.h, MQ_NSUMS). Summing that single buffer across ranks and
@@ -20,6 +21,7 @@ host never blocks.
 import ctypes
 import hashlib
 import os
+import weakref
 
 import numpy as np
 import torch
@@ -70,14 +72,42 @@ def _t_len(batch):
     return int(getattr(batch, "t_len", batch.max_seq_length))
 
 
+# fields whose sampled rows are digested: what the loss reads (q_learner.py:39-44, 58-86; coma_learner.py:32-46)
+DIGEST_FIELDS = ("reward", "actions", "terminated", "filled", "avail_actions", "obs", "state")
+_MIX = -7046029254386353131   # 0x9E3779B97F4A7C15 as int64 (golden-ratio multiplier); products wrap mod 2^64
+
+
+def content_digest(batch):
+    """64-bit digest of the CONTENTS of the sampled transitions (the fields the learner reads, DIGEST_FIELDS), computed
+    where the batch lives (device kernels for a GPU replay, one host read-back). Every element's bit pattern is mixed
+    with its position and the sum wraps in int64, so the result does not depend on the summation order: two ranks get
+    the same digest exactly when their sampled rows are bitwise equal (up to hash collisions)."""
+    acc = 0
+    for k in DIGEST_FIELDS:
+        try:
+            v = batch[k]
+        except (KeyError, TypeError):
+            continue
+        if v.dtype == torch.float32:
+            v = v.contiguous().view(torch.int32)
+        v = v.reshape(-1).to(torch.int64)
+        pos = torch.arange(1, v.numel() + 1, dtype=torch.int64, device=v.device)
+        x = (v + pos) * _MIX
+        x = x ^ (x >> 29)          # arithmetic shift: deterministic for negative values too
+        acc = (acc * 31 + int((x * _MIX).sum().item())) & 0xFFFFFFFFFFFFFFFF
+    return acc
+
+
 def batch_fingerprint(batch):
-    """63-bit fingerprint of what a rank is about to train on: batch size, t_len and the sampled episode ids (a
-    SampledBatch, dense or not, keeps them; a plain EpisodeBatch contributes its shape only)."""
+    """63-bit fingerprint of what a rank is about to train on: batch size, t_len, the sampled episode ids (a
+    SampledBatch, dense or not, keeps them) and the digest of the sampled rows' contents (content_digest), so ranks
+    that draw the same ids from replay buffers whose contents differ (diverged rollouts, run.py:203-204) disagree."""
     h = hashlib.blake2b(digest_size=8)
     h.update(np.asarray([batch.batch_size, _t_len(batch)], dtype=np.int64).tobytes())
     ids = getattr(batch, "ep_ids_np", None)
     if ids is not None:
         h.update(np.ascontiguousarray(ids, dtype=np.int64).tobytes())
+    h.update(np.asarray([content_digest(batch)], dtype=np.uint64).tobytes())
     return int.from_bytes(h.digest(), "little") >> 1
 
 
@@ -91,9 +121,42 @@ def check_same_batch(batch, device, group=None):
     hi, lo = int(t[0].item()), -int(t[1].item())
     if hi != fp or lo != fp:
         raise _lib.MQError(
-            "data-parallel learner: the ranks passed different batches to train() (batch {} episodes, t_len {}). "
-            "Every rank must pass the same GLOBAL sample (same seed, so ReplayBuffer.sample draws the same ids); "
-            "the learner shards it itself".format(batch.batch_size, _t_len(batch)))
+            "data-parallel learner: the ranks passed different batches to train() (batch {} episodes, t_len {}; "
+            "the sampled ids or the contents of the sampled episodes differ). Every rank must pass the same GLOBAL "
+            "sample from the same replay contents (same seed, so ReplayBuffer.sample draws the same ids); the "
+            "learner shards it itself".format(batch.batch_size, _t_len(batch)))
+
+
+class DPCheck:
+    """When a data-parallel train() runs check_same_batch. The decision depends only on the call count, which is the
+    same on every rank (ranks that made different numbers of train() calls would already disagree on the gradient
+    all-reduce), so every rank enters the check's collective together — never one rank alone. `learner_dp_check`:
+    "first" (the first call only), "always", "off", or an int N (calls 0, N, 2N, ...; the default is 100, which costs
+    one small all-reduce and a digest every 100 steps)."""
+    DEFAULT_EVERY = 100
+
+    def __init__(self, mode):
+        if mode is None:
+            mode = self.DEFAULT_EVERY
+        if isinstance(mode, str) and mode.isdigit():
+            mode = int(mode)
+        if not (mode in ("first", "always", "off") or (isinstance(mode, int) and mode > 0)):
+            raise ValueError("learner_dp_check must be 'first', 'always', 'off' or a positive int, not {!r}"
+                             .format(mode))
+        self.mode = mode
+        self.calls = 0
+        self.done = 0
+
+    def due(self):
+        """Whether this call checks; advances the call counter."""
+        c, self.calls = self.calls, self.calls + 1
+        if self.mode == "always":
+            return True
+        if self.mode == "off":
+            return False
+        if self.mode == "first":
+            return c == 0
+        return c % self.mode == 0
 
 
 def local_shard(batch, rank, world, check=True, device="cpu", group=None):
@@ -113,15 +176,21 @@ def local_shard(batch, rank, world, check=True, device="cpu", group=None):
 class SharedComm:
     """One RCCL communicator per process (mq_comm_create), created once on first use (rank 0's id broadcast over
     torch.distributed) and lent to every learner handle with mq_comm_use / mc_comm_use. Handles never free it, so a
-    handle rebuilt mid-run (larger batch or episode) re-attaches without a collective."""
+    handle rebuilt mid-run (larger batch or episode) re-attaches without a collective. The handles that borrowed it
+    are tracked: free() detaches them first (mq_comm_detach / mc_comm_detach), so none is left holding a destroyed
+    communicator; a learner that trains again afterwards re-attaches to a new one (`generation` changed)."""
     _comm = None
     _key = None
+    generation = 0
+    _borrowers = []   # (weakref to the Handle / ComaHandle, detach function name)
 
     @classmethod
     def get(cls, lib, device):
         from .. import _lib
         key = (torch.device(device).index, dist.get_world_size(), id(dist.group.WORLD))
         if cls._comm is None or cls._key != key:
+            if cls._comm is not None:
+                cls.free()
             uid = broadcast_comm_id(lib, device)
             comm = ctypes.c_void_p()
             _lib.check(lib.mq_comm_create(uid, dist.get_rank(), dist.get_world_size(), ctypes.byref(comm)))
@@ -129,12 +198,32 @@ class SharedComm:
         return cls._comm
 
     @classmethod
+    def lend(cls, handle, use, detach, device):
+        """Attach the process communicator to `handle` (a _lib.Handle / ComaHandle) with `use` (mq_comm_use /
+        mc_comm_use) and remember to detach it (`detach`) before the communicator is freed."""
+        from .. import _lib
+        comm = cls.get(handle.lib, device)
+        _lib.check(getattr(handle.lib, use)(handle.h, comm))
+        cls._borrowers = [(r, d) for r, d in cls._borrowers if r() is not None]
+        cls._borrowers.append((weakref.ref(handle), detach))
+        handle.native = True
+        handle.comm_gen = cls.generation
+
+    @classmethod
     def free(cls):
-        """Release the communicator (call after the last train() and before destroy_process_group)."""
+        """Release the communicator (call after the last train() and before destroy_process_group). Every handle
+        that still borrows it is detached first and falls back to `native = False` until it re-attaches."""
         if cls._comm is not None:
             from .. import _lib
+            for ref, detach in cls._borrowers:
+                h = ref()
+                if h is not None and getattr(h, "h", None) and h.h.value:
+                    getattr(h.lib, detach)(h.h)
+                    h.native = False
+            cls._borrowers = []
             _lib.load().mq_comm_free(cls._comm)
             cls._comm = cls._key = None
+            cls.generation += 1
 
 
 def shard_bounds(batch_size, rank, world):

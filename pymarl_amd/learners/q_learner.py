@@ -8,7 +8,8 @@ device buffers. There is no CPU path: a learner that is not on a HIP device rais
 
 Data parallel: with `args.learner_dp = True` and torch.distributed initialised (RCCL, one process
 per GPU), every rank calls train() with the SAME GLOBAL sample, as run.py:207-219 does unchanged (ranks share the
-seed, so the sampled ids agree; checked once, `args.learner_dp_check`); the learner trains its own contiguous shard
+seed, so the sampled ids agree; ids and contents checked on a call-count schedule, `args.learner_dp_check`); the
+learner trains its own contiguous shard
 of the episodes (dp.local_shard), the unnormalised gradient buffer (+ the loss/mask sums in its tail) is summed with
 ONE all_reduce, and every rank then applies the identical normalised update. Under an RCCL process group the learner
 borrows the process's library communicator (dp.SharedComm: mq_comm_create once, mq_comm_use per handle): the
@@ -29,7 +30,7 @@ from torch.optim import RMSprop
 from .. import _lib
 from ..components.episode_buffer import is_replay_view
 from ..modules.flat import pack, rebind
-from .dp import SharedComm, allreduce_grad_buffer, dp_world, local_shard, native_comm_wanted
+from .dp import DPCheck, SharedComm, allreduce_grad_buffer, dp_world, local_shard, native_comm_wanted
 from ..modules.mixers.qmix import QMixer
 from ..modules.mixers.vdn import VDNMixer
 
@@ -151,10 +152,9 @@ class QLearner:
         self.target_mac = copy.deepcopy(mac)
         self.log_stats_t = -self.args.learner_log_interval - 1
         self.dp = bool(getattr(args, "learner_dp", False))
-        # "first" (default): check that the ranks passed the same global sample on the first data-parallel train()
-        # and whenever its shape changes; "always": every train(); "off"
-        self.dp_check = getattr(args, "learner_dp_check", "first")
-        self._dp_checked = None
+        # when to check that the ranks passed the same global sample (ids AND contents): a call-count schedule, the
+        # same on every rank (dp.DPCheck: "first", "always", "off" or every N calls, default 100)
+        self.dp_check = DPCheck(getattr(args, "learner_dp_check", None))
 
         # flat device buffers: [agent params | mixer params] for online and target nets (MQ_P_* order)
         self._mods = [m for m in (self.mac.agent, self.mixer) if m is not None and len(list(m.parameters()))]
@@ -208,11 +208,9 @@ class QLearner:
         """Data parallel: this rank's shard of the global sample (dp.local_shard), the ranks' agreement checked per
         `self.dp_check`."""
         rank, world = dp_world()
-        key = (batch.batch_size, getattr(batch, "t_len", batch.max_seq_length), world)
-        check = self.dp_check == "always" or (self.dp_check != "off" and self._dp_checked != key)
+        check = self.dp_check.due()
         out = local_shard(batch, rank, world, check=check, device=self._online.device)
-        if check:
-            self._dp_checked = key
+        self.dp_check.done += int(check)
         return out
 
     def _get_handle(self, batch):
@@ -220,6 +218,8 @@ class QLearner:
         world = dp_world()[1] if self._dp_active() else 1
         need_b = max(batch.batch_size, -(-getattr(self.args, "batch_size", 1) // world))
         key = (need_b, T)
+        if self._handle is not None and self._handle.native and self._handle.comm_gen != SharedComm.generation:
+            self._handle = None   # its communicator was freed (SharedComm.free detached it): rebuild and re-attach
         if self._handle is None or self._handle_key[0] < need_b or self._handle_key[1] < T:
             cfg = make_config(self.args, MIXER_IDS[self.args.mixer], input_dim=self.mac.agent.input_dim,
                               max_batch=need_b, max_seq=T)
@@ -232,8 +232,7 @@ class QLearner:
             h.native = False
             if self._dp_active() and native_comm_wanted(self._online.device):
                 # the process's communicator, created once (a handle rebuilt later needs no collective to attach)
-                _lib.check(h.lib.mq_comm_use(h.h, SharedComm.get(h.lib, self._online.device)))
-                h.native = True
+                SharedComm.lend(h, "mq_comm_use", "mq_comm_detach", self._online.device)
             if h.n_params != self.n_params:
                 raise _lib.MQError("parameter layout mismatch: library {} vs modules {}".format(h.n_params,
                                                                                               self.n_params))

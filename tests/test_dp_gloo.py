@@ -83,7 +83,7 @@ def _contract_worker(rank, world, port, out_path):
     try:
         from pymarl_amd import _lib
         from pymarl_amd.components.episode_buffer import SampledBatch
-        from pymarl_amd.learners.dp import local_shard, shard_bounds
+        from pymarl_amd.learners.dp import DPCheck, local_shard, shard_bounds
         from tests.golden_utils import Case
         from tests.gpu_helpers import build
         case = Case("cfg2_qmix_ragged")
@@ -95,7 +95,7 @@ def _contract_worker(rank, world, port, out_path):
         loc = learner._local_batch(gb)
         lo, hi = shard_bounds(len(ids), rank, world)
         res["ids_ok"] = bool(np.array_equal(loc.ep_ids_np, ids[lo:hi]) and loc.t_len == gb.t_len)
-        res["checked"] = learner._dp_checked is not None
+        res["checked"] = learner.dp_check.done == 1
         # an already-sharded batch (the old caller-shards contract) is rejected, never sharded twice
         try:
             learner._local_batch(gb.shard(rank, world))
@@ -120,8 +120,30 @@ def _contract_worker(rank, world, port, out_path):
             res["mismatch"] = "accepted"
         except _lib.MQError:
             res["mismatch"] = "raised"
-        # "first": the check is not repeated for the same shape; "always" repeats it
-        learner.dp_check = "always"
+        # equal ids over DIFFERENT replay contents (ranks whose rollouts diverged): every rank raises
+        rew = buf.data.transition_data["reward"]
+        saved = rew[ids[1], 2].clone()
+        if rank == 1:
+            rew[ids[1], 2] += 0.5
+        try:
+            local_shard(SampledBatch(buf, ids)[:, :gb.t_len], rank, world, check=True)
+            res["contents"] = "accepted"
+        except _lib.MQError:
+            res["contents"] = "raised"
+        rew[ids[1], 2] = saved
+        # the schedule is a call count, the same on every rank: rank-local shape differences never make one rank
+        # enter the check's collective alone; the next scheduled call catches them on every rank
+        learner.dp_check = DPCheck(2)
+        sched = []
+        for call in range(4):
+            t_len = gb.t_len - (call % 2) * rank    # rank 1 truncates differently on the unchecked calls
+            try:
+                learner._local_batch(SampledBatch(buf, ids)[:, :t_len])
+                sched.append("ok")
+            except _lib.MQError:
+                sched.append("raised")
+        res["schedule"] = sched
+        learner.dp_check = DPCheck("always")
         try:
             learner._local_batch(SampledBatch(buf, ids if rank == 0 else ids[::-1].copy())[:, :gb.t_len])
             res["always"] = "accepted"
@@ -150,5 +172,70 @@ def test_dp_train_contract_global_sample(tmp_path):
     for r in range(2):
         res = json.loads(str(np.load(out.format(r))[0]))
         assert res == {"ids_ok": True, "checked": True, "reshard": "rejected", "reshard_t": "rejected",
-                       "dense_ok": True, "mismatch": "raised", "always": "raised", "tiny": "rejected",
+                       "dense_ok": True, "mismatch": "raised", "contents": "raised",
+                       "schedule": ["ok", "ok", "ok", "ok"], "always": "raised", "tiny": "rejected",
                        "cpu_train": "raised"}, (r, res)
+
+
+def test_dp_check_schedule():
+    from pymarl_amd.learners.dp import DPCheck
+    c = DPCheck(None)
+    assert [c.due() for _ in range(201)].count(True) == 3          # calls 0, 100, 200
+    c = DPCheck(3)
+    assert [c.due() for _ in range(7)] == [True, False, False, True, False, False, True]
+    c = DPCheck("first")
+    assert [c.due() for _ in range(3)] == [True, False, False]
+    assert [DPCheck("off").due() for _ in range(2)] == [False, False]
+    assert DPCheck("5").mode == 5
+    with pytest.raises(ValueError):
+        DPCheck("sometimes")
+
+
+def test_content_digest_sees_contents():
+    from pymarl_amd.components.episode_buffer import SampledBatch
+    from pymarl_amd.learners.dp import batch_fingerprint, content_digest
+    from tests.golden_utils import Case
+    from tests.gpu_helpers import build
+    case = Case("tiny_qmix")
+    _, buf, _, _, _ = build(case, device="cpu")
+    ids = case.z["ids"][0]
+    a = SampledBatch(buf, ids)
+    d0, f0 = content_digest(a), batch_fingerprint(a)
+    assert d0 == content_digest(SampledBatch(buf, ids)) and f0 == batch_fingerprint(SampledBatch(buf, ids))
+    obs = buf.data.transition_data["obs"]
+    obs[ids[0], 1, 0, 0] = th.nextafter(obs[ids[0], 1, 0, 0], th.tensor(1e9))   # one ulp in one element
+    assert content_digest(a) != d0 and batch_fingerprint(a) != f0
+    # the dense (materialised) batch of the same rows has the same digest
+    assert content_digest(a.materialize()) == content_digest(a)
+
+
+def test_shared_comm_free_detaches_borrowers():
+    import ctypes
+    from pymarl_amd.learners.dp import SharedComm
+
+    class _Lib:
+        def __init__(self):
+            self.calls = []
+
+        def mq_comm_detach(self, h):
+            self.calls.append(("mq", h.value))
+            return 0
+
+        def mc_comm_detach(self, h):
+            self.calls.append(("mc", h.value))
+            return 0
+
+    class _H:
+        def __init__(self, lib, v):
+            self.lib, self.h, self.native = lib, ctypes.c_void_p(v), True
+
+    lib = _Lib()
+    a, b = _H(lib, 16), _H(lib, 32)
+    gen = SharedComm.generation
+    SharedComm._comm = ctypes.c_void_p(None)    # mq_comm_free(NULL) is a no-op
+    SharedComm._borrowers = []
+    import weakref
+    SharedComm._borrowers += [(weakref.ref(a), "mq_comm_detach"), (weakref.ref(b), "mc_comm_detach")]
+    SharedComm.free()
+    assert lib.calls == [("mq", 16), ("mc", 32)]
+    assert not a.native and not b.native and SharedComm._comm is None and SharedComm.generation == gen + 1

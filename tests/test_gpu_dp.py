@@ -56,6 +56,7 @@ def _worker(rank, world, port, out_path):
         th.cuda.synchronize()
         from pymarl_amd import _lib
         from pymarl_amd.components.episode_buffer import SampledBatch
+        from pymarl_amd.learners.dp import DPCheck
         p_before = learner._online.detach().cpu().numpy().copy()
         gb = SampledBatch(buf, case.z["ids"][0])
         try:   # a pre-sharded batch (the old caller-shards contract) is rejected, not sharded twice
@@ -63,7 +64,7 @@ def _worker(rank, world, port, out_path):
             rec["reshard"] = 0
         except ValueError:
             rec["reshard"] = 1
-        learner.dp_check = "always"
+        learner.dp_check = DPCheck("always")
         try:   # ranks that pass different samples raise together (collective check), before any kernel runs
             learner.train(SampledBatch(buf, case.z["ids"][0] if rank == 0 else case.z["ids"][1]), 0, 0)
             rec["mismatch"] = 0

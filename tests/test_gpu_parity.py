@@ -459,34 +459,6 @@ def test_data_parallel_norm_path_single_rank(cases):
     assert abs(outs[1][1] - outs[0][1]) <= 1e-5 * abs(outs[0][1])
 
 
-@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg2_qmix_ragged", "cfg2_qmix_nodq", "cfg1_qmix", "tiny_qmix_full",
-                                  "rw2_qmix"])
-def test_hymix_bitwise(cases, name, monkeypatch):
-    """The QMIX hypernet and mixer in one launch (hymix_kernel, MQ_HYMIX=1) equal hyper_ws_kernel followed by
-    mix_fast_kernel (the default, MQ_HYMIX=0) bit for bit: parameters, gradients, square_avg, stats and the double-Q
-    actions over up to four steps (ragged episodes, double_q False, M not a multiple of 16, the row-tile agent)."""
-    from tests.gpu_helpers import build, flat_grads, flat_params
-    case = get_case(cases, name)
-    monkeypatch.setenv("MQ_HYP_IN_FWD", "0")
-    outs = []
-    for hm in ("1", "0"):
-        monkeypatch.setenv("MQ_HYMIX", hm)
-        args, buf, mac, learner, logger = build(case)
-        np.random.seed(case.sampler_seed)
-        for k in range(min(4, len(case.episodes))):
-            batch = buf.sample(case.B)
-            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
-        th.cuda.synchronize()
-        assert learner.last_plan()["hyper"] == ("ws_mix" if hm == "1" else "ws"), learner.last_plan()
-        outs.append((flat_params(learner), flat_grads(learner), learner._sq.cpu().numpy(), learner.last_stats(),
-                     learner.last_cur_max_actions().cpu().numpy()))
-    for a, b in zip(outs[0], outs[1]):
-        if isinstance(a, dict):
-            assert a == b
-        else:
-            assert np.array_equal(a, b)
-
-
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg4_qmix", "cfg1_qmix", "tiny_qmix_full", "cfg2_qmix_ragged"])
 def test_hyper_in_forward_grid_bitwise(cases, name, monkeypatch):
     """The QMIX hypernet as workgroups appended to the fused forward's grid (MQ_HYP_IN_FWD=1; the default for shards
@@ -495,7 +467,6 @@ def test_hyper_in_forward_grid_bitwise(cases, name, monkeypatch):
     two-wave forward of configs[3]'s shard (cfg4) included."""
     from tests.gpu_helpers import build, flat_grads, flat_params
     case = get_case(cases, name)
-    monkeypatch.setenv("MQ_HYMIX", "0")   # both arms feed mix_fast_kernel from HYP
     outs = []
     for inf in ("1", "0"):
         monkeypatch.setenv("MQ_HYP_IN_FWD", inf)
@@ -537,23 +508,3 @@ def test_dwh_in_bptt_grid_bitwise(cases, name, monkeypatch):
     assert outs[0][3] == outs[1][3]
 
 
-def test_dwh_split_clamped_when_fused(cases, monkeypatch):
-    """MQ_DWH_SPLIT above kRedZ = 16: the fused dW_hyper + reduction-pass-1 launch clamps its m-slices to 16 (its
-    slabs must go straight to pass 2, never read by pass-1 blocks of the same grid), so the result is bitwise the
-    split-16 run's, and both match the oracle teacher-forced."""
-    from tests.gpu_helpers import build, flat_grads, flat_params
-    case = get_case(cases, "cfg2_qmix")
-    outs = []
-    for split in ("32", "16"):
-        monkeypatch.setenv("MQ_DWH_SPLIT", split)
-        args, buf, mac, learner, logger = build(case)
-        np.random.seed(case.sampler_seed)
-        for k in range(2):
-            batch = buf.sample(case.B)
-            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
-        th.cuda.synchronize()
-        outs.append((flat_params(learner), flat_grads(learner), learner.last_stats()))
-    assert np.array_equal(outs[0][0], outs[1][0])
-    assert np.array_equal(outs[0][1], outs[1][1])
-    monkeypatch.setenv("MQ_DWH_SPLIT", "32")
-    run_teacher_forced(case, 2, False, monkeypatch)
