@@ -292,8 +292,10 @@ CASES = {
     "rw4_vdn": dict(WIDE, n=16, A=7, O=10, S=16, T=10, B=80, n_episodes=100, mixer="vdn"),
     "wide_qmix": dict(WIDE, n=8, A=5, O=8, S=12, T=8, B=300, n_episodes=320, mixer="qmix"),
     # BASELINE configs[2] exactly (27m_vs_30m shape, VDN, B = 128): R = 3456 rows, the bench's kernel path
-    "cfg3_vdn_b128": dict(CFG3, mixer="vdn", B=128, n_episodes=136, steps=2, episodes=[0, 8], ragged=True,
-                          record_actions_steps=1),
+    # 6 steps with a target update at step 3 (episodes 16 -> 200): the row-tile kernels hold the reference's
+    # free-running trajectory past an update
+    "cfg3_vdn_b128": dict(CFG3, mixer="vdn", B=128, n_episodes=136, steps=6, episodes=[0, 8, 16, 200, 208, 216],
+                          ragged=True, record_actions_steps=2),
     "tiny_qmix_full": dict(TINY, mixer="qmix", ragged=False, n_episodes=4, steps=3, episodes=[0, 200, 201]),
     "cfg2_qmix": dict(CFG2, mixer="qmix"),
     "cfg2_vdn": dict(CFG2, mixer="vdn", steps=10, episodes=[8 * k for k in range(5)] + [200 + k for k in range(5)]),
@@ -303,7 +305,7 @@ CASES = {
     # the same shape under QMIX: S=1170 exercises the hypernet / dW_hyper kernels at a long K
     "cfg3_qmix": dict(CFG3, mixer="qmix", steps=3, episodes=[0, 8, 200], store_params=False),
     # BASELINE configs[3] shape (2s3z, QMIX): one rank's shard of B=512 over 8 GPUs, R = 64*5 = 320 rows > 256
-    "cfg4_qmix": dict(CFG4, mixer="qmix"),
+    "cfg4_qmix": dict(CFG4, mixer="qmix", steps=8, episodes=[0, 8, 16, 24, 200, 208, 216, 224]),
     # the reference branches no shipped config takes: double_q: False (q_learner.py:77-78), obs_last_action /
     # obs_agent_id: False (basic_controller.py:111-120, 150-153)
     "tiny_qmix_nodq": dict(TINY, mixer="qmix", double_q=False),
