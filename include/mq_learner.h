@@ -143,10 +143,10 @@ int mq_qmix_forward(const float* mixer, int32_t n_agents, int32_t state_dim, int
 /* Which kernel variants the last mq_forward_backward launched (test / profiling introspection; no device sync).
  * rw_fwd / rw_bwd: rows per workgroup of the unfused recurrences (0 when the fused kernel ran). */
 enum { MQ_HYP_NONE = 0, MQ_HYP_WS = 1, MQ_HYP_LDS = 2, MQ_HYP_GEMM = 3 };
-enum { MQ_MIX_FAST16 = 0, MQ_MIX_FAST32 = 1, MQ_MIX_GENERIC = 2 };
+enum { MQ_MIX_FAST16 = 0, MQ_MIX_FAST32 = 1, MQ_MIX_GENERIC = 2, MQ_MIX_STREAM = 3 };
 typedef struct mq_plan {
   int32_t rows;          /* R = batch_size * n_agents */
-  int32_t fused_fwd;     /* gru_fwd_fused_kernel (1) or fc1 / gi / gru_fwd<rw_fwd> / fc2 (0) */
+  int32_t fused_fwd;     /* gru_fwd_fused_kernel (1), gru_fwd_pair_kernel (2) or fc1 / gi / gru_fwd<rw_fwd> / fc2 (0) */
   int32_t rw_fwd;
   int32_t fused_bwd;     /* gru_bwd_fused_kernel (1) or gru_bwd<rw_bwd> / dx1 / dw1 (0) */
   int32_t rw_bwd;

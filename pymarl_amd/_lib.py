@@ -86,7 +86,7 @@ class MQPlan(ctypes.Structure):
 
 
 HYP_NAMES = {0: "none", 1: "ws", 2: "lds", 3: "gemm"}
-MIX_NAMES = {0: "fast16", 1: "fast32", 2: "generic"}
+MIX_NAMES = {0: "fast16", 1: "fast32", 2: "generic", 3: "stream"}
 
 INLINE_IDS = 256   # MQ_INLINE_IDS: batches up to this size pass their episode ids in the kernel arguments
 COMM_ID_BYTES = 128   # MQ_COMM_ID_BYTES (ncclUniqueId)

@@ -45,6 +45,17 @@ MQ_DEV float qmix_fwd_lane(const float* hyp, const float* qs_lds, const float* V
   return y;
 }
 
+// STREAM (mix_stream_ok: n * A <= MIXS_MAX): the selection's operands — the four items' Q rows at t+1 (one
+// contiguous run of 4 n A floats when B % 4 == 0) and their avail rows — are staged by the whole workgroup with
+// coalesced loads, every load in flight at once, masked on the way into LDS; each agent lane then scans its row
+// from LDS. The generic form has every agent lane walk its own row in global memory (A-strided 4-byte loads,
+// ceil(A / 12) dependent rounds), which held configs[2]'s mixer (n = 27, A = 36) at 2 TB/s. Same comparisons in the
+// same order: identical outputs.
+constexpr int MIXS_MAX = 1024;   // n * A staged per item
+constexpr int MIXS_NPT = MIXS_MAX / 256;
+inline bool mix_stream_ok(int n, int A) { return n * A <= MIXS_MAX; }
+
+template <bool STREAM>
 __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* __restrict__ P0,
                                                   const float* __restrict__ P1, Lay L, Work w, int32_t* curmax_out) {
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -65,8 +76,55 @@ __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* _
   }
   const float* Qon = w.Q;
   const float* Qtg = w.Q + d.RT() * A;
-  // ---- chosen action values and double-Q target selection (q_learner.py:55, 68-78); lane = agent
   float chosen = 0.0f, tmax = 0.0f;
+  if constexpr (STREAM) {
+    __shared__ float qm[4 * MIXS_MAX];      // the four items' masked selection rows [item][agent][action]
+    __shared__ uint8_t avs[4 * MIXS_MAX];   // their avail bits
+    const int nA = n * A;
+    const float* qsel_base = d.double_q ? Qon : Qtg;
+    float qv[4][MIXS_NPT];
+    int32_t avv[4][MIXS_NPT];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {   // every load of the block first
+      const int mi = min((int)blockIdx.x * 4 + it, d.M - 1);
+      const int ti = (int)fdiv((uint32_t)mi, d.dB), bi = mi - ti * d.B;
+      const float* qrow = qsel_base + ((int64_t)(ti + 1) * R + (int64_t)bi * n) * A;
+      const int32_t* arow = rp.avail + ((rp.ep(bi) * d.t_stride + ti + 1) * n) * (int64_t)A;
+#pragma unroll
+      for (int k = 0; k < MIXS_NPT; ++k) {
+        const int e = min((int)threadIdx.x + 256 * k, nA - 1);
+        qv[it][k] = qrow[e];
+        avv[it][k] = arow[e];
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < 4; ++it)
+#pragma unroll
+      for (int k = 0; k < MIXS_NPT; ++k) {
+        const int e = threadIdx.x + 256 * k;
+        if (e < nA) {
+          qm[it * nA + e] = avv[it][k] ? qv[it][k] : kNegMask;
+          avs[it * nA + e] = avv[it][k] ? 1 : 0;
+        }
+      }
+    __syncthreads();
+    if (valid && lane < n) {
+      const int r = b * n + lane;
+      const int at = (int)rp.actions[(ep * d.t_stride + t) * n + lane];
+      chosen = Qon[((int64_t)t * R + r) * A + at];
+      const float* row = qm + wv * nA + lane * A;
+      float best = 0.0f;
+      int cur = 0;
+      for (int a = 0; a < A; ++a) {
+        const float v = row[a];
+        if (a == 0 || v > best) { best = v; cur = a; }
+      }
+      if (d.double_q) tmax = avs[wv * nA + lane * A + cur] ? Qtg[((int64_t)(t + 1) * R + r) * A + cur] : kNegMask;
+      else tmax = best;
+      if (curmax_out) curmax_out[(int64_t)t * R + r] = cur;
+    }
+  } else
+  // ---- chosen action values and double-Q target selection (q_learner.py:55, 68-78); lane = agent
   if (valid && lane < n) {
     const int r = b * n + lane;
     const int64_t slot = ep * d.t_stride + t;

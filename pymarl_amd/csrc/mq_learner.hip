@@ -26,6 +26,7 @@
 #include "learner_gemms.hpp"
 #include "gru_kernels.hpp"
 #include "gru_fwd_fused.hpp"
+#include "gru_fwd_pair.hpp"
 #include "gru_bwd_fused.hpp"
 #include "gru_tiles.hpp"
 #include "mix_kernels.hpp"
@@ -112,6 +113,12 @@ struct mq_handle {
   // dW_hyper's tiles appended to the fused BPTT's grid (gru_bwd_fused.hpp, DWH = 1) when its rows exceed the CUs
   // (a second wave of rows leaves CUs idle); MQ_DWH_IN_BWD=0 never, =1 always (A/B switches; bitwise either way)
   int dwh_in_bwd = getenv("MQ_DWH_IN_BWD") ? atoi(getenv("MQ_DWH_IN_BWD")) : -1;
+  // the row-pair forward (gru_fwd_pair.hpp: both nets of a row in one workgroup, one per CU) when the rows fit one
+  // wave of workgroups; MQ_FWD_PAIR=0 keeps the one-row-net kernel, =1 forces the pair (A/B switches)
+  int fwd_pair = getenv("MQ_FWD_PAIR") ? atoi(getenv("MQ_FWD_PAIR")) : -1;
+  bool pair_split = !(getenv("MQ_PAIR_SPLIT") && atoi(getenv("MQ_PAIR_SPLIT")) == 0);   // roles on disjoint SIMDs
+  // MQ_MIX_GENERIC=1: mix_kernel<false> where mix_kernel<true> (staged selection rows) would run (A/B switch)
+  bool mix_generic = getenv("MQ_MIX_GENERIC") != nullptr;
   int num_cu = 0;
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
   int slots = 0;
@@ -468,9 +475,21 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     const bool two_waves = device_cus(h) > 0 && d.R > h->num_cu;   // 2R row-nets at two per CU
     hyp_in_fwd = (h->hyp_in_fwd == 1 || (h->hyp_in_fwd < 0 && two_waves)) && c.mixer == MQ_MIXER_QMIX &&
                  hyper_ws_ok(d.S, d.E, d.NH, d.M) && hyf_ok(d.S, d.E, d.NH, d.M);
+    const bool pair = !hyp_in_fwd && (h->fwd_pair == 1 || (h->fwd_pair < 0 && !two_waves && device_cus(h) > 0)) &&
+                      pair_fwd_ok(d.I, d.O, d.A, d.n, RT);
     if (hyp_in_fwd) {
       plan.hyper = MQ_HYP_WS;
       launch_fwd_fused_hyp(s, d, rp, (const float*)h->on, (const float*)h->tg, L, w);
+    } else if (pair) {
+      plan.fused_fwd = 2;
+      const char* stamp_path = getenv("MQ_PAIR_STAMP");   // diagnostic: step stamps of the first 8 workgroups
+      launch_fwd_pair(s, d, rp, (const float*)h->on, (const float*)h->tg, L, w, h->pair_split, stamp_path != nullptr);
+      if (stamp_path && FCH * d.O <= 256 * 5) {
+        std::vector<uint32_t> st((size_t)8 * 3 * d.Tp);
+        MQ_HIP(hipMemcpyAsync(st.data(), w.slab_rnn, st.size() * 4, hipMemcpyDeviceToHost, s));
+        MQ_HIP(hipStreamSynchronize(s));
+        if (FILE* f = fopen(stamp_path, "ab")) { fwrite(st.data(), 4, st.size(), f); fclose(f); }
+      }
     } else {
       launch_fwd_fused(dim3(d.R, 2), s, d, rp, (const float*)h->on, (const float*)h->tg, L, w);
     }
@@ -527,15 +546,20 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
   pt.begin(PH_MIX);
   {
     const bool fast = d.n <= 16 && d.E <= 64;   // mix_kernel serves the rest (n > 16 or A > 32)
-    plan.mix = fast && d.A <= 16 ? MQ_MIX_FAST16 : fast && d.A <= 32 ? MQ_MIX_FAST32 : MQ_MIX_GENERIC;
+    const bool stream = mix_stream_ok(d.n, d.A) && !h->mix_generic;
+    plan.mix = fast && d.A <= 16 ? MQ_MIX_FAST16 : fast && d.A <= 32 ? MQ_MIX_FAST32 : stream ? MQ_MIX_STREAM
+                                                                                             : MQ_MIX_GENERIC;
     if (fast && d.A <= 16)
       hipLaunchKernelGGL((mix_fast_kernel<16, 16>), dim3(h->nblk_mix), dim3(256), 0, s, d, rp, (const float*)h->on,
                          (const float*)h->tg, L, w, curmax);
     else if (fast && d.A <= 32)
       hipLaunchKernelGGL((mix_fast_kernel<32, 16>), dim3(h->nblk_mix), dim3(256), 0, s, d, rp, (const float*)h->on,
                          (const float*)h->tg, L, w, curmax);
+    else if (stream)
+      hipLaunchKernelGGL(mix_kernel<true>, dim3(h->nblk_mix), dim3(256), 0, s, d, rp, (const float*)h->on,
+                         (const float*)h->tg, L, w, curmax);
     else
-      hipLaunchKernelGGL(mix_kernel, dim3(h->nblk_mix), dim3(256), 0, s, d, rp, (const float*)h->on,
+      hipLaunchKernelGGL(mix_kernel<false>, dim3(h->nblk_mix), dim3(256), 0, s, d, rp, (const float*)h->on,
                          (const float*)h->tg, L, w, curmax);
     MQ_HIP(hipGetLastError());
   }

@@ -222,8 +222,8 @@ WIDE_PLANS = {
     "rw2_qmix": dict(rows=576, tiles=1, fused_fwd=0, fused_bwd=0, inline_ids=1, hyper="ws"),
     "rw4_vdn": dict(rows=1280, tiles=1, fused_fwd=0, fused_bwd=0, inline_ids=1, mix="fast16"),
     "wide_qmix": dict(rows=2400, tiles=1, fused_fwd=0, fused_bwd=0, inline_ids=0),
-    "cfg3_vdn_b128": dict(rows=3456, tiles=1, fused_fwd=0, fused_bwd=0, inline_ids=1, mix="generic"),
-    "cfg2_iql": dict(rows=256, fused_fwd=1, fused_bwd=1, hyper="none"),
+    "cfg3_vdn_b128": dict(rows=3456, tiles=1, fused_fwd=0, fused_bwd=0, inline_ids=1, mix="stream"),
+    "cfg2_iql": dict(rows=256, fused_fwd=2, fused_bwd=1, hyper="none"),
     # configs[3]'s per-GPU shard: R = 320 rows, past the CU count, still on the fused BPTT (a second wave of rows)
     "cfg4_qmix": dict(rows=320, fused_fwd=1, fused_bwd=1, hyper="ws"),
 }
@@ -350,6 +350,18 @@ def test_teacher_forced_steps(cases, name, steps, unfused, monkeypatch):
         assert plan["tiles"] == 1 and plan["fused_fwd"] == 0 and plan["fused_bwd"] == 0, plan
 
 
+@pytest.mark.parametrize("name,steps", [("cfg2_qmix", 3), ("cfg2_qmix_ragged", 3), ("tiny_vdn", 3),
+                                        ("tiny_qmix_bare", 3), ("cfg1_qmix", 3)])
+@pytest.mark.parametrize("pair", ["0", "1"])
+def test_forward_pair_switch_teacher_forced(cases, name, steps, pair, monkeypatch):
+    """Both one-wave agent forwards teacher-forced against the oracle: the row-pair kernel (gru_fwd_pair.hpp, both nets
+    of a row per workgroup; the default when the rows fit the CUs) and the one-row-net kernel it replaced there
+    (MQ_FWD_PAIR=0; still the forward past one wave of rows, e.g. configs[3]'s shard)."""
+    monkeypatch.setenv("MQ_FWD_PAIR", pair)
+    learner = run_teacher_forced(get_case(cases, name), steps, False, monkeypatch)
+    assert learner.last_plan()["fused_fwd"] == (2 if pair == "1" else 1)
+
+
 @pytest.mark.parametrize("name,steps,flow", [
     ("tiny_qmix", 4, "cpu_to"), ("cfg2_qmix", 3, "cpu_to"), ("cfg2_qmix_ragged", 3, "cpu_to"), ("cfg1_qmix", 4, "cpu_to"),
     ("tiny_vdn", 3, "cpu_to"), ("tiny_qmix", 4, "dense_slice"), ("cfg1_qmix", 4, "dense_slice")])
@@ -468,6 +480,7 @@ def test_hyper_in_forward_grid_bitwise(cases, name, monkeypatch):
     from tests.gpu_helpers import build, flat_grads, flat_params
     case = get_case(cases, name)
     outs = []
+    monkeypatch.setenv("MQ_FWD_PAIR", "0")   # both arms on the one-row-net forward (the pair kernel has no HYP grid)
     for inf in ("1", "0"):
         monkeypatch.setenv("MQ_HYP_IN_FWD", inf)
         args, buf, mac, learner, logger = build(case)
@@ -482,6 +495,31 @@ def test_hyper_in_forward_grid_bitwise(cases, name, monkeypatch):
     assert np.array_equal(outs[0][1], outs[1][1])
     assert np.array_equal(outs[0][2], outs[1][2])
     assert outs[0][3] == outs[1][3]
+
+
+@pytest.mark.parametrize("name", ["cfg3_vdn", "cfg3_qmix", "cfg3_vdn_b128"])
+def test_mix_stream_bitwise(cases, name, monkeypatch):
+    """configs[2]'s mixer with the selection rows staged by the workgroup (mix_kernel<true>, the default where
+    n * A <= 1024) equals the per-lane generic form (MQ_MIX_GENERIC=1) bitwise, double-Q argmax included."""
+    from tests.gpu_helpers import build, flat_grads, flat_params
+    case = get_case(cases, name)
+    outs = []
+    for gen in ("0", "1"):
+        if gen == "1":
+            monkeypatch.setenv("MQ_MIX_GENERIC", "1")
+        else:
+            monkeypatch.delenv("MQ_MIX_GENERIC", raising=False)
+        args, buf, mac, learner, logger = build(case)
+        np.random.seed(case.sampler_seed)
+        for k in range(min(2, len(case.episodes))):
+            batch = buf.sample(case.B)
+            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
+        th.cuda.synchronize()
+        assert learner.last_plan()["mix"] == ("generic" if gen == "1" else "stream")
+        outs.append((flat_params(learner), flat_grads(learner), learner.last_stats()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]
 
 
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg4_qmix", "cfg1_qmix", "tiny_qmix_full"])
