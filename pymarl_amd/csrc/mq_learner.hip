@@ -115,8 +115,7 @@ struct mq_handle {
   int dwh_in_bwd = getenv("MQ_DWH_IN_BWD") ? atoi(getenv("MQ_DWH_IN_BWD")) : -1;
   // the row-pair forward (gru_fwd_pair.hpp: both nets of a row in one workgroup, one per CU) when the rows fit one
   // wave of workgroups; MQ_FWD_PAIR=0 keeps the one-row-net kernel, =1 forces the pair (A/B switches)
-  int fwd_pair = getenv("MQ_FWD_PAIR") ? atoi(getenv("MQ_FWD_PAIR")) : -1;
-  bool pair_split = !(getenv("MQ_PAIR_SPLIT") && atoi(getenv("MQ_PAIR_SPLIT")) == 0);   // roles on disjoint SIMDs
+  int fwd_pair = getenv("MQ_FWD_PAIR") ? atoi(getenv("MQ_FWD_PAIR")) : 0;   // TEMP default off until GPU-verified
   // MQ_MIX_GENERIC=1: mix_kernel<false> where mix_kernel<true> (staged selection rows) would run (A/B switch)
   bool mix_generic = getenv("MQ_MIX_GENERIC") != nullptr;
   int num_cu = 0;
@@ -473,17 +472,23 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     // one row per workgroup: fc1 / W_ih / fc2 ride on the recurrence's idle matrix cores (gru_fwd_fused.hpp)
     pt.begin(PH_GRUF);
     const bool two_waves = device_cus(h) > 0 && d.R > h->num_cu;   // 2R row-nets at two per CU
-    hyp_in_fwd = (h->hyp_in_fwd == 1 || (h->hyp_in_fwd < 0 && two_waves)) && c.mixer == MQ_MIXER_QMIX &&
+    // the row-pair forward when the rows fit one wave of workgroups (MQ_FWD_PAIR=1 forces it, =0 keeps the one-row-net
+    // kernel); MQ_HYP_IN_FWD=1 asks for the one-row-net kernel with the hypernet appended to its grid
+    const bool pair = h->hyp_in_fwd != 1 && pair_fwd_ok(d.I, d.O, d.A, d.n, RT) &&
+                      (h->fwd_pair == 1 || (h->fwd_pair < 0 && !two_waves && device_cus(h) > 0));
+    hyp_in_fwd = !pair && (h->hyp_in_fwd == 1 || (h->hyp_in_fwd < 0 && two_waves)) && c.mixer == MQ_MIXER_QMIX &&
                  hyper_ws_ok(d.S, d.E, d.NH, d.M) && hyf_ok(d.S, d.E, d.NH, d.M);
-    const bool pair = !hyp_in_fwd && (h->fwd_pair == 1 || (h->fwd_pair < 0 && !two_waves && device_cus(h) > 0)) &&
-                      pair_fwd_ok(d.I, d.O, d.A, d.n, RT);
     if (hyp_in_fwd) {
       plan.hyper = MQ_HYP_WS;
       launch_fwd_fused_hyp(s, d, rp, (const float*)h->on, (const float*)h->tg, L, w);
     } else if (pair) {
       plan.fused_fwd = 2;
+      // the QMIX hypernet as the pair kernel's epilogue (MQ_HYP_IN_FWD=0 keeps hyper_ws_kernel after it)
+      hyp_in_fwd = h->hyp_in_fwd != 0 && c.mixer == MQ_MIXER_QMIX && hyper_ws_ok(d.S, d.E, d.NH, d.M) &&
+                   hyf_ok(d.S, d.E, d.NH, d.M);
+      if (hyp_in_fwd) plan.hyper = MQ_HYP_WS;
       const char* stamp_path = getenv("MQ_PAIR_STAMP");   // diagnostic: step stamps of the first 8 workgroups
-      launch_fwd_pair(s, d, rp, (const float*)h->on, (const float*)h->tg, L, w, h->pair_split, stamp_path != nullptr);
+      launch_fwd_pair(s, d, rp, (const float*)h->on, (const float*)h->tg, L, w, hyp_in_fwd, stamp_path != nullptr);
       if (stamp_path && FCH * d.O <= 256 * 5) {
         std::vector<uint32_t> st((size_t)8 * 3 * d.Tp);
         MQ_HIP(hipMemcpyAsync(st.data(), w.slab_rnn, st.size() * 4, hipMemcpyDeviceToHost, s));

@@ -1,21 +1,19 @@
-"""Decode the row-pair forward's step stamps (MQ_PAIR_STAMP=<file>, gru_fwd_pair.hpp STAMP): per chunk phase p, the
-mean cycles from the previous barrier release to the recurrence wave's / producer wave's arrival, and the step period.
-Usage: python scripts/pair_stamps.py <file> <Tp>"""
+"""Decode the row-pair forward's stamps (MQ_PAIR_STAMP=<file>, gru_fwd_pair.hpp STAMP) of the last train(): the
+recurrence's cycles per step inside a chunk, across a chunk boundary, and how early or late the producers reach each
+chunk barrier relative to the recurrence. Usage: python scripts/pair_stamps.py <file> <Tp>"""
 import sys
 import numpy as np
 
 path, Tp = sys.argv[1], int(sys.argv[2])
 a = np.fromfile(path, dtype=np.uint32)
-rec = 8 * 3 * Tp
-a = a[-rec:].reshape(8, 3, Tp).astype(np.int64)   # last train(): [block][release, rec arrival, prod arrival][t]
-rel, arr_r, arr_p = a[:, 0], a[:, 1], a[:, 2]
-per = np.diff(rel, axis=1)                        # step t period (t >= 1)
-rb = arr_r[:, 1:] - rel[:, :-1]                   # recurrence work of step t
-pb = arr_p[:, 1:] - rel[:, :-1]                   # producer work of step t
-print("mean step period %.0f cycles (median %.0f), first release -> last %.0f cycles" %
-      (per.mean(), np.median(per), (rel[:, -1] - rel[:, 0]).mean()))
-print(" p  period  rec_busy  prod_busy")
+a = a[-8 * 3 * Tp:].reshape(8, 3, Tp).astype(np.int64)   # [block][step end, rec chunk arrival, prod chunk arrival][t]
+end, arr_r, arr_p = a[:, 0], a[:, 1], a[:, 2]
+per = np.diff(end, axis=1)                                # cycles of step t (t >= 1)
 t = np.arange(1, Tp)
-for p in range(16):
-    sel = (t % 16) == p
-    print("%2d  %6.0f  %8.0f  %9.0f" % (p, per[:, sel].mean(), rb[:, sel].mean(), pb[:, sel].mean()))
+inside, first = per[:, (t % 16) != 0], per[:, (t % 16) == 0]
+last = np.arange(15, Tp, 16)
+print("steps inside a chunk: mean %.0f, median %.0f cycles; first step of a chunk: mean %.0f" %
+      (inside.mean(), np.median(inside), first.mean()))
+print("whole T loop %.0f cycles (%d steps)" % ((end[:, -1] - end[:, 0]).mean(), Tp))
+print("producer arrival - recurrence arrival at each chunk barrier (cycles, + = producers late):")
+print(" ", np.round((arr_p[:, last] - arr_r[:, last]).mean(0)).astype(int).tolist())

@@ -497,6 +497,34 @@ def test_hyper_in_forward_grid_bitwise(cases, name, monkeypatch):
     assert outs[0][3] == outs[1][3]
 
 
+@pytest.mark.parametrize("name", ["cfg2_qmix", "cfg1_qmix", "tiny_qmix_full", "cfg2_qmix_ragged"])
+def test_pair_hyper_epilogue_bitwise(cases, name, monkeypatch):
+    """The QMIX hypernet as the row-pair forward's epilogue (the default with the pair kernel) equals hyper_ws_kernel
+    launched after the forward (MQ_HYP_IN_FWD=0) bitwise: parameters, gradients, square_avg and stats over up to
+    four steps, ragged M included."""
+    from tests.gpu_helpers import build, flat_grads, flat_params
+    case = get_case(cases, name)
+    outs = []
+    monkeypatch.setenv("MQ_FWD_PAIR", "1")
+    for inf in (None, "0"):
+        if inf is None:
+            monkeypatch.delenv("MQ_HYP_IN_FWD", raising=False)
+        else:
+            monkeypatch.setenv("MQ_HYP_IN_FWD", inf)
+        args, buf, mac, learner, logger = build(case)
+        np.random.seed(case.sampler_seed)
+        for k in range(min(4, len(case.episodes))):
+            batch = buf.sample(case.B)
+            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
+        th.cuda.synchronize()
+        assert learner.last_plan()["hyper"] == "ws" and learner.last_plan()["fused_fwd"] == 2
+        outs.append((flat_params(learner), flat_grads(learner), learner._sq.cpu().numpy(), learner.last_stats()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert np.array_equal(outs[0][2], outs[1][2])
+    assert outs[0][3] == outs[1][3]
+
+
 @pytest.mark.parametrize("name", ["cfg3_vdn", "cfg3_qmix", "cfg3_vdn_b128"])
 def test_mix_stream_bitwise(cases, name, monkeypatch):
     """configs[2]'s mixer with the selection rows staged by the workgroup (mix_kernel<true>, the default where
