@@ -26,53 +26,216 @@
 
 namespace mq {
 
+constexpr int PSP = H + 4;   // pitch of a W_hh / W_ih row staged in LDS during the prologue
+
 struct alignas(16) PairLds {
   float h0[H];                    // init_hidden: zeros
+  float xin[2][FCH][FXP];         // [chunk & 1] agent inputs (both nets)
+  // from here on, the prologue's weight staging area ([net][192 rows][PSP]) overlays the T loop's buffers
   float hs[2][2][FCH][H + 4];     // [net][chunk & 1][step][unit]: h_t (the recurrence's h_{t-1}, fc2's operand)
   float gi[2][2][FCH][G3];        // [net][chunk & 1][step][gate column]
-  float xin[2][FCH][FXP];         // [chunk & 1] agent inputs (both nets)
   float x1[2][2][FCH][H + 4];     // [net][chunk & 1] X1
+  f32x4 grec[2][FCH][H];          // [chunk & 1][step][unit] online gate record (r, z, n, W_hn h + b_hn)
 };
+static_assert(sizeof(PairLds) - offsetof(PairLds, hs) >= 2 * G3 * PSP * sizeof(float), "weight staging fits");
 
 inline bool pair_fwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_fwd_ok(I, O, A, n, RT); }
 
-// STAMP (diagnostic, MQ_PAIR_STAMP): lane 0 of recurrence wave 0 and of producer 0 in the first 8 workgroups write
-// s_memtime into w.slab_rnn as uint32 [block][3][Tp]: 0 the end of each step (recurrence), 1 the recurrence's
-// chunk-barrier arrival, 2 the producers' chunk-barrier arrival (both at the chunk's last step).
-template <int NG, bool STAMP>
+// STAMP (diagnostic, MQ_PAIR_STAMP; Tp <= 512): s_memtime stamps of the first 8 workgroups (cdna_hip_programming.md
+// §7 form: s_memtime + lgkmcnt(0) in one asm statement), kept in LDS and written to w.slab_rnn as uint32
+// [block][16 + 2 * 512] at the end: [0] kernel entry, [1] recurrence loop start, [2] its end, [3] producers'
+// prologue done, [4] the hypernet epilogue's end, producers' [5] loads issued, [6] loads landed, [7] X1(0..1) done,
+// [8] GI(0) done, [9] recurrence's W_hh landed; [16 + t] the recurrence's step t end; [16 + 512 + t] the producers'
+// arrival at the barrier closing the chunk of step t (chunk ends only).
+constexpr int PST = 16 + 2 * 512;
+MQ_DEV uint32_t stamp_now() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return (uint32_t)t;
+}
+// ---- HYP = 2: the QMIX hypernet (qmix.py:30-44) for block hb = r (32 state rows of net hb & 1) on waves 4 and 5,
+// which otherwise only pass barriers. Those waves share SIMDs s0 / s1 with the recurrences, whose matrix cores are
+// idle; in the prologue the recurrences themselves wait for the producers' first chunks (~25k cycles, stamps), so the
+// hypernet's MFMAs mostly fill dead time there, and the rest is spread thinly over the T loop's chunks. Wave hw owns
+// N-tiles hw, hw + 2, .. of NH / 16, both 16-row M-tiles each; the A operand (states, zero K padding) is staged once
+// in LDS, the B fragments come straight from the parameters (one tile ahead, in registers). Operand maps, K order and
+// bias add are hyper_ws_kernel's: HYP and S0 are bitwise its outputs.
+constexpr int HT_SP = 4 * 48 + 4;   // row pitch of the staged states (K padded to 192, zeros)
+// tiles a wave has finished by the end of the interval that barrier i (0 = S1) opens: none before S3 (W_ih staging),
+// then 1, 2 and 2 in the prologue intervals, the rest spread over the chunks
+MQ_DEV int hyp_tiles_by(int i, int cnt, int nchunks) {
+  constexpr int kPro[4] = {0, 1, 3, 5};
+  if (i < 2) return 0;
+  if (i < 6) return min(cnt, kPro[i - 2]);
+  const int rem = max(cnt - kPro[3], 0), c = i - 5;   // chunk c - 1 done
+  return min(cnt, kPro[3] + (rem * c + nchunks - 1) / nchunks);
+}
+template <bool STAMP, class StageWih>
+MQ_DEV void hyper_waves(const Dims& d, const Rep& rp, const float* __restrict__ P0, const float* __restrict__ P1,
+                        const Lay& L, const Work& w, float* hst, uint32_t* stl, int nbar, StageWih stage_wih) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  const int hw = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) - 4;
+  const int hb = blockIdx.x, S = d.S, NH = d.NH, E = d.E, nE = d.n * d.E;
+  const bool act = hb < 2 * ((d.M + 31) / 32);   // the host launches HYP = 2 only when every block has a row
+  const int z = hb & 1, m0 = (hb >> 1) * 32;
+  const float* __restrict__ P = z ? P1 : P0;
+  const int NT = NH / 16, cnt = act ? (NT - hw + 1) / 2 : 0, nchunks = nbar - 6;
+  // states: wave hw gathers rows 16 hw .. 16 hw + 15 (lanes: columns l, l + 64, l + 128) and stages them
+  if (act) {
+    float vs[16][3];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = min(m0 + 16 * hw + i, d.M - 1), t = (int)fdiv((uint32_t)m, d.dB), b = m - t * d.B;
+      const float* row = rp.state + (rp.ep(b) * d.t_stride + t + z) * (int64_t)S;
+#pragma unroll
+      for (int cg = 0; cg < 3; ++cg) vs[i][cg] = row[min(lane + 64 * cg, S - 1)];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int ii = 16 * hw + i, m = m0 + ii;
+#pragma unroll
+      for (int cg = 0; cg < 3; ++cg) {
+        const int col = lane + 64 * cg;
+        const float v = (col < S && m < d.M) ? vs[i][cg] : 0.0f;
+        hst[ii * HT_SP + col] = v;
+        if (z == 0 && w.S0 && m < d.M && col < S) w.S0[(int64_t)m * S + col] = v;
+      }
+    }
+  }
+  lds_barrier();   // S2: states staged (read after S3)
+  stage_wih();
+  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)P, (short)0, (int)(L.o[MQ_P_COUNT] * sizeof(float)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(w.HYP + (int64_t)z * d.M * NH), (short)0, (int)((int64_t)d.M * NH * sizeof(float)), 0x00020000);
+  f32x4 ba[12], bb[12];
+  float bja = 0.0f, bjb = 0.0f;
+  auto fetch = [&](int k, f32x4 (&bf)[12], float& bj) {   // B fragments of local tile k: row j, columns 48 g ..
+    const int j = 16 * (hw + 2 * k) + c16;
+    const HypSeg sg = hyp_seg(L, nE, E, j);
+    const int base = (int)(sg.w + (int64_t)sg.row * S) * 4 + 192 * g;
+#pragma unroll
+    for (int mm = 0; mm < 12; ++mm)
+      bf[mm] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, base + 16 * mm, 0, 0));
+    bj = P[sg.b + sg.row];
+  };
+  const float* a0 = hst + c16 * HT_SP + 48 * g;
+  const float* a1 = a0 + 16 * HT_SP;
+  auto tile = [&](int k, const f32x4 (&bf)[12], float bj) {
+    f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+#pragma unroll
+    for (int mm = 0; mm < 12; ++mm) {
+      const f32x4 av0 = *(const f32x4*)&a0[4 * mm];
+      const f32x4 av1 = *(const f32x4*)&a1[4 * mm];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc0 = mfma16x4(av0[e], bf[mm][e], acc0);
+        acc1 = mfma16x4(av1[e], bf[mm][e], acc1);
+      }
+    }
+    const int ob0 = ((m0 + 4 * g) * NH + 16 * (hw + 2 * k) + c16) * 4, ob1 = ob0 + 16 * NH * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc0[e] + bj), ors, ob0, e * NH * 4, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc1[e] + bj), ors, ob1, e * NH * 4, 0);
+    }
+  };
+  if (cnt > 0) fetch(0, ba, bja);
+  int done = 0;
+  for (int i = 2; i < nbar; ++i) {
+    lds_barrier();   // barrier i (S3 .. the last chunk's)
+    const int upto = hyp_tiles_by(i, cnt, nchunks);
+    while (done < upto) {   // wave-uniform
+      if (done & 1) {
+        if (done + 1 < cnt) fetch(done + 1, ba, bja);
+        tile(done, bb, bjb);
+      } else {
+        if (done + 1 < cnt) fetch(done + 1, bb, bjb);
+        tile(done, ba, bja);
+      }
+      ++done;
+    }
+    if constexpr (STAMP) {
+      if (hw == 0 && i >= 2 && i < 6) { const uint32_t v = stamp_now(); if (lane == 0) stl[9 + i] = v; }
+    }
+  }
+  if constexpr (STAMP) { const uint32_t v = stamp_now(); if (hw == 0 && lane == 0) stl[15] = v; }
+}
+
+template <int NG, bool STAMP, int HYP = 0>
 MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0, const float* __restrict__ P1,
-                      const Lay& L, const Work& w, PairLds& S) {
+                      const Lay& L, const Work& w, PairLds& S, uint32_t* stl, float* hst = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int R = d.R, Tp = d.Tp, I = d.I, O = d.O, A = d.A, n = d.n;
   const int cl = (Tp - 1) / FCH;   // last chunk
   const int r = blockIdx.x;
   const uint32_t RH = (uint32_t)R * H;
-  uint32_t* const stp = (uint32_t*)w.slab_rnn + (size_t)blockIdx.x * 3 * Tp;
-  auto stamp = [&](int k, int t) {
-    if (STAMP && lane == 0 && blockIdx.x < 8) stp[k * Tp + t] = (uint32_t)__builtin_amdgcn_s_memtime();
+  auto stamp = [&](int slot) {
+    if constexpr (STAMP) {
+      const uint32_t v = stamp_now();
+      if (lane == 0) stl[slot] = v;
+    }
   };
 
   if (tid < H) S.h0[tid] = 0.0f;
-  constexpr int kPrologueBarriers = 3;
+  constexpr int kPrologueBarriers = 6;
   const bool producer = (wv & 2) != 0;
+  // Every workgroup needs both nets' W_hh (recurrences) and W_ih (producers) in registers in a lane layout whose direct
+  // loads hit 32-64 cache lines per instruction; through L1 that took ~15k cycles at the kernel's start (stamps,
+  // round 5). So they are read with coalesced 16-byte loads (a wave covers 1 KB per instruction), staged in LDS
+  // ([net][row][PSP], over the T loop's buffers), and picked up from there: W_hh by all waves before barrier S1, W_ih
+  // by the producer and idle waves between S2 and S3.
+  float* const stg = &S.hs[0][0][0][0];
+  // (each workgroup starts at a different sixteenth of the rows, so the 256 CUs do not request the same L2 lines at
+  // the same time)
+  const int srot = (int)(blockIdx.x & 15);
+  auto stage_rows = [&](int o_param, int nthr, int t0) {   // [2 nets][192][64] floats from P0 / P1 at o_param
+    constexpr int NV = 2 * G3 * H / 4;
+    for (int e0 = 0; e0 < NV; e0 += 16 * nthr) {
+      f32x4 v[16];
+      int ev[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        ev[q] = e0 + t0 + nthr * ((q + srot) & 15);
+        const int e = min(ev[q], NV - 1), z = e >= NV / 2, rem = 4 * (e - z * (NV / 2));
+        v[q] = *(const f32x4*)((z ? P1 : P0) + o_param + rem);
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int e = ev[q], z = e >= NV / 2, rem = 4 * (e - z * (NV / 2));
+        if (e < NV) *(f32x4*)&stg[(z * G3 + (rem >> 6)) * PSP + (rem & 63)] = v[q];
+      }
+    }
+  };
+  stage_rows((int)L.o[MQ_P_RNN_W_HH], 512, tid);
+  lds_barrier();   // S1: W_hh staged
 
   if (!producer) {
-    if (wv >= 2) {   // waves 4, 5: the recurrence SIMDs' second slots stay free of work; they pass the barriers
-      for (int i = 0; i < kPrologueBarriers + cl + 1; ++i) lds_barrier();
+    if (wv >= 2) {   // waves 4, 5 (the recurrence SIMDs' second slots)
+      if constexpr (HYP == 2) {
+        hyper_waves<STAMP>(d, rp, P0, P1, L, w, hst, stl, kPrologueBarriers + cl + 1,
+                           [&]() { stage_rows((int)L.o[MQ_P_RNN_W_IH], 384, 64 * (wv - 4) + lane); });
+        return;
+      }
+      lds_barrier();   // S2
+      stage_rows((int)L.o[MQ_P_RNN_W_IH], 384, 64 * (wv - 4) + lane);   // with the producers: threads 0..127 of 384
+      for (int i = 2; i < kPrologueBarriers + cl + 1; ++i) lds_barrier();
       return;
     }
     // ================================================================ recurrence wave of net z (wave z)
     const int z = wv, j = lane;
     const float* __restrict__ P = z ? P1 : P0;
-    f32x2 wr[32], wz[32], wn[32];   // W_hh[gate * 64 + j][2 k, 2 k + 1]
+    f32x2 wr[32], wz[32], wn[32];   // W_hh[gate * 64 + j][2 k, 2 k + 1], from the staged rows
     {
-      const float* Whh = P + L.o[MQ_P_RNN_W_HH];
+      const float* Whh = stg + (z * G3 + j) * PSP;
 #pragma unroll
       for (int k4 = 0; k4 < 16; ++k4) {
-        const f32x4 a = *(const f32x4*)(Whh + (int64_t)(0 * H + j) * H + 4 * k4);
-        const f32x4 b = *(const f32x4*)(Whh + (int64_t)(1 * H + j) * H + 4 * k4);
-        const f32x4 c = *(const f32x4*)(Whh + (int64_t)(2 * H + j) * H + 4 * k4);
+        const f32x4 a = *(const f32x4*)(Whh + (0 * H) * PSP + 4 * k4);
+        const f32x4 b = *(const f32x4*)(Whh + (1 * H) * PSP + 4 * k4);
+        const f32x4 c = *(const f32x4*)(Whh + (2 * H) * PSP + 4 * k4);
         wr[2 * k4] = f32x2{a[0], a[1]}; wr[2 * k4 + 1] = f32x2{a[2], a[3]};
         wz[2 * k4] = f32x2{b[0], b[1]}; wz[2 * k4 + 1] = f32x2{b[2], b[3]};
         wn[2 * k4] = f32x2{c[0], c[1]}; wn[2 * k4 + 1] = f32x2{c[2], c[3]};
@@ -81,10 +244,11 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
     const float bhr = P[L.o[MQ_P_RNN_B_HH] + j], bhz = P[L.o[MQ_P_RNN_B_HH] + H + j],
                 bhn = P[L.o[MQ_P_RNN_B_HH] + 2 * H + j];
     drain_vmem();
-    for (int i = 0; i < kPrologueBarriers; ++i) lds_barrier();
+    if (z == 0) stamp(9);
+    for (int i = 1; i < kPrologueBarriers; ++i) lds_barrier();   // S2 (W_hh copied out) .. S6
     const bool online = z == 0;
     float hprev = 0.0f;
-    const uint32_t hlo = ((uint32_t)r * H + j) * 4, glo = ((uint32_t)r * (4 * H) + j) * 4;
+    if (z == 0) stamp(1);
     __builtin_amdgcn_s_setprio(2);
     for (int c = 0; c <= cl; ++c) {
       const int pend = min(FCH, Tp - FCH * c);
@@ -115,20 +279,14 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
         const float h1 = (hprev - ng) * zg + ng;
         hprev = h1;
         S.hs[z][c & 1][p][j] = h1;   // read back by this wave's next step (in-order LDS, no barrier)
-        if (online) {
-          buf_st(buf_rsrc(w.Hs + (int64_t)t * RH), hlo, h1);
-          const auto gb = buf_rsrc(w.Gates + (int64_t)t * (4 * RH));
-          buf_st(gb, glo, rg);
-          buf_st(gb, glo + 4 * H, zg);
-          buf_st(gb, glo + 8 * H, ng);
-          buf_st(gb, glo + 12 * H, ghn);
-        }
-        if (z == 0) stamp(0, t);
+        // the online record goes to HBM through the producers (one chunk later), not from this wave
+        if (online) S.grec[c & 1][p][j] = f32x4{rg, zg, ng, ghn};
+        if (z == 0) stamp(16 + t);
       }
-      if (z == 0) stamp(1, FCH * c + pend - 1);
       lds_barrier();   // chunk c's h history complete; chunk c + 1's GI staged
     }
     __builtin_amdgcn_s_setprio(0);
+    if (z == 0) stamp(2);
     return;
   }
 
@@ -162,25 +320,27 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
     a_ld = *(const int*)(rp.actions + (slot0 + t) * n + ag);
   };
   issue_gather(0);
-  // register-resident weights of both nets: W1 (fc1 B fragments of N-tile pw), W_ih (3 N-tiles), W2 (K = 64)
+  // register-resident weights of both nets: W1 (fc1 B fragments of N-tile pw), W_ih (3 N-tiles), W2 (K = 64), as
+  // 16-byte loads (W_ih / W2 rows are 64 floats at offsets that are multiples of 4; W1's rows when I % 4 == 0,
+  // otherwise element by element), every load of the prologue in flight at once
   float w1r[2][FKQ], wih[2][3][16], w2r[16], bih[2][3], b1[2], b2;
 #pragma unroll
   for (int z = 0; z < 2; ++z) {
     const float* __restrict__ P = z ? P1 : P0;
-    const float* W1 = P + L.o[MQ_P_FC1_W] + (int64_t)(16 * pw + c16) * I;
+    const float* W1 = P + L.o[MQ_P_FC1_W] + (int64_t)(16 * pw + c16) * I + g * Kq;
+    if ((I & 3) == 0) {
 #pragma unroll
-    for (int k = 0; k < FKQ; ++k) {
-      const int kk = g * Kq + k;
-      w1r[z][k] = (k < Kq && kk < I) ? W1[min(kk, I - 1)] : 0.0f;
+      for (int m = 0; m < FKQ / 4; ++m) {
+        const f32x4 v = 4 * m < Kq ? *(const f32x4*)(W1 + 4 * m) : f32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w1r[z][4 * m + e] = (g * Kq + 4 * m + e < I) ? v[e] : 0.0f;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < FKQ; ++k) w1r[z][k] = (k < Kq && g * Kq + k < I) ? W1[min(k, I - 1 - g * Kq)] : 0.0f;
     }
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const int nn = 16 * (3 * pw + s) + c16;
-      const float* Wi = P + L.o[MQ_P_RNN_W_IH] + (int64_t)nn * H + 16 * g;
-#pragma unroll
-      for (int kb = 0; kb < 16; ++kb) wih[z][s][kb] = Wi[kb];
-      bih[z][s] = P[L.o[MQ_P_RNN_B_IH] + nn];
-    }
+    for (int s = 0; s < 3; ++s) bih[z][s] = P[L.o[MQ_P_RNN_B_IH] + 16 * (3 * pw + s) + c16];
     b1[z] = P[L.o[MQ_P_FC1_B] + 16 * pw + c16];
   }
   {
@@ -188,7 +348,11 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
     const float* __restrict__ P = zf ? P1 : P0;
     const float* W2 = P + L.o[MQ_P_FC2_W] + (int64_t)min(c16, A - 1) * H + 16 * g;
 #pragma unroll
-    for (int kb = 0; kb < 16; ++kb) w2r[kb] = c16 < A ? W2[kb] : 0.0f;
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = *(const f32x4*)(W2 + 4 * q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w2r[4 * q + e] = c16 < A ? v[e] : 0.0f;
+    }
     b2 = c16 < A ? P[L.o[MQ_P_FC2_B] + c16] : 0.0f;
   }
 
@@ -282,69 +446,131 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
       buf_st(qb, (t0 + 4 * g + e < Tp && c16 < A) ? (lo + e * RA) * 4 : kDrop, (q0[e] + q1[e]) + b2);
   };
 
-  // ---- prologue (3 barriers, matched by the other waves): xin(0), xin(1) -> X1(0), X1(1) -> GI(0); xin(2) staged
+  // the online net's h and gate records of chunk cc (LDS hs[0] / grec, written by the recurrence) -> Hs / Gates:
+  // 16 steps x 64 units; thread (step 4 k + (ptid >> 6), unit ptid & 63), coalesced along the units
+  auto store_records = [&](int cc) {
+    const int t0 = FCH * cc, j = ptid & 63;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = 4 * k + (ptid >> 6), t = t0 + i;
+      const f32x4 gv = S.grec[cc & 1][i][j];
+      const float hv = S.hs[0][cc & 1][i][j];
+      const bool ok = t < Tp;
+      buf_st(buf_rsrc(w.Hs + (int64_t)min(t, Tp - 1) * RH), ok ? ((uint32_t)r * H + j) * 4 : kDrop, hv);
+      const auto gb = buf_rsrc(w.Gates + (int64_t)min(t, Tp - 1) * (4 * RH));
+      const uint32_t go = ((uint32_t)r * (4 * H) + j) * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) buf_st(gb, ok ? go + q * 4 * H : kDrop, gv[q]);
+    }
+  };
+
+  // ---- prologue (barriers S2 .. S6 after S1, matched by the other waves): W_ih staged and picked up, xin(0),
+  // xin(1) -> X1(0), X1(1) -> GI(0); xin(2) staged
+  if (pw == 0) stamp(5);
+  lds_barrier();   // S2: the recurrences have copied W_hh out of the staging area
+  stage_rows((int)L.o[MQ_P_RNN_W_IH], 384, 128 + ptid);
   drain_vmem();
+  if (pw == 0) stamp(6);
   store_gather(0);
-  if (cl >= 1) { issue_gather(1); drain_vmem(); store_gather(1); }
+  if (cl >= 1) issue_gather(1);
+  lds_barrier();   // S3: W_ih staged
+#pragma unroll
+  for (int z = 0; z < 2; ++z)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const float* Wi = stg + (z * G3 + 16 * (3 * pw + s) + c16) * PSP + 16 * g;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 v = *(const f32x4*)(Wi + 4 * q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) wih[z][s][4 * q + e] = v[e];
+      }
+    }
+  if (cl >= 1) { drain_vmem(); store_gather(1); }
   if (cl >= 2) issue_gather(2);
-  lds_barrier();   // 1: xin(0), xin(1), h0
+  if (pw == 0) stamp(3);
+  lds_barrier();   // S4: W_ih copied out (the staging area is free), xin(0), xin(1)
 #pragma unroll
   for (int z = 0; z < 2; ++z) {
     fc1(z, 0);
     if (cl >= 1) fc1(z, 1);
   }
-  lds_barrier();   // 2: X1(0), X1(1); xin(0) free
+  if (pw == 0) stamp(7);
+  lds_barrier();   // S5: X1(0), X1(1); xin(0) free
   if (cl >= 2) { store_gather(2); if (cl >= 3) issue_gather(3); }
 #pragma unroll
   for (int z = 0; z < 2; ++z) gi(z, 0);
-  lds_barrier();   // 3: GI(0), xin(2)
+  if (pw == 0) stamp(8);
+  lds_barrier();   // S6: GI(0), xin(2)
 
   for (int c = 0; c <= cl; ++c) {
     // chunk c: the recurrences run steps 16 c .. 16 c + 15 meanwhile
-    if (c >= 1 && pw < 2) fc2(c - 1);
+    if (c >= 1) {
+      if (pw < 2) fc2(c - 1);
+      store_records(c - 1);
+    }
     if (c + 1 <= cl) { gi(0, c + 1); gi(1, c + 1); }
     if (c + 2 <= cl) { fc1(0, c + 2); fc1(1, c + 2); }
     if (c + 3 <= cl) { store_gather(c + 3); if (c + 4 <= cl) issue_gather(c + 4); }
-    if (pw == 0) stamp(2, min(FCH * c + FCH - 1, Tp - 1));
+    if (pw == 0) stamp(16 + 512 + min(FCH * c + FCH - 1, Tp - 1));
     lds_barrier();
   }
   if (pw < 2) fc2(cl);   // the last chunk's h history is complete after the final barrier
+  store_records(cl);
 }
 
-// HYP = 1: the QMIX hypernet as the forward's epilogue. Once a workgroup's row is done, its whole CU (all eight
-// waves, the LDS) runs hyper_fwd_body for hypernet block r, r + R, .. (32 state rows of one net each): the fp32 MFMA
-// work of hyper_ws_kernel (bitwise its HYP and S0) without its launch, and on CUs whose matrix cores the recurrence
-// SIMDs left idle.
+// HYP = 1: the QMIX hypernet as the forward's epilogue: once a workgroup's row is done, its CU runs hyper_fwd_body
+// (gru_fwd_fused.hpp) for hypernet blocks r, r + R, .. — for grids with more blocks than rows. HYP = 2: blocks on
+// waves 4 / 5 during the prologue and T loop (hyper_waves above), one block per workgroup.
 template <int NG, bool STAMP = false, int HYP = 0>
 __global__ __launch_bounds__(512, 1) void gru_fwd_pair_kernel(Dims d, Rep rp, const float* __restrict__ P0,
                                                               const float* __restrict__ P1, Lay L, Work w) {
   __shared__ PairLds S;
   static_assert(sizeof(PairLds) >= hyf_floats() * sizeof(float), "the hypernet epilogue reuses the forward's LDS");
-  pair_body<NG, STAMP>(d, rp, P0, P1, L, w, S);
-  if constexpr (HYP != 0) {
+  __shared__ uint32_t stl[STAMP ? PST : 1];
+  __shared__ float hst[HYP == 2 ? 32 * HT_SP : 1];
+  if constexpr (STAMP) {
+    const uint32_t t0 = stamp_now();
+    if (threadIdx.x == 0) stl[0] = t0;
+  }
+  pair_body<NG, STAMP, HYP>(d, rp, P0, P1, L, w, S, stl, hst);
+  if constexpr (HYP == 1) {
     const int nhb = 2 * ((d.M + 31) / 32);
     for (int hb = blockIdx.x; hb < nhb; hb += gridDim.x) {
       __syncthreads();   // the row's (or the previous block's) last LDS reads are done
       hyper_fwd_body(d, rp, P0, P1, L, w.HYP, w.S0, (float*)&S, hb);
     }
   }
+  if constexpr (STAMP) {
+    __syncthreads();
+    const uint32_t te = stamp_now();
+    if (threadIdx.x == 0) stl[4] = te;
+    __syncthreads();
+    if (blockIdx.x < 8)
+      for (int i = threadIdx.x; i < PST; i += 512) ((uint32_t*)w.slab_rnn)[(size_t)blockIdx.x * PST + i] = stl[i];
+  }
 }
 
 // Host: the row-pair forward, grid R, with the smallest gather-slot instantiation that covers O.
 inline void launch_fwd_pair(hipStream_t s, const Dims& d, const Rep& rp, const float* P0, const float* P1,
-                            const Lay& L, const Work& w, bool hyp, bool stamp = false) {
+                            const Lay& L, const Work& w, int hyp, bool stamp = false) {
   const dim3 g(d.R), b(512);
   const bool g5 = FCH * d.O <= 256 * 5;
+#define MQ_PAIR_LAUNCH(NG, ST, HY) hipLaunchKernelGGL((gru_fwd_pair_kernel<NG, ST, HY>), g, b, 0, s, d, rp, P0, P1, L, w)
   if (stamp) {
-    if (hyp) hipLaunchKernelGGL((gru_fwd_pair_kernel<5, true, 1>), g, b, 0, s, d, rp, P0, P1, L, w);
-    else hipLaunchKernelGGL((gru_fwd_pair_kernel<5, true, 0>), g, b, 0, s, d, rp, P0, P1, L, w);
-  } else if (hyp) {
-    if (g5) hipLaunchKernelGGL((gru_fwd_pair_kernel<5, false, 1>), g, b, 0, s, d, rp, P0, P1, L, w);
-    else hipLaunchKernelGGL((gru_fwd_pair_kernel<FGATHER, false, 1>), g, b, 0, s, d, rp, P0, P1, L, w);
+    if (hyp == 2) MQ_PAIR_LAUNCH(5, true, 2);
+    else if (hyp == 1) MQ_PAIR_LAUNCH(5, true, 1);
+    else MQ_PAIR_LAUNCH(5, true, 0);
+  } else if (g5) {
+    if (hyp == 2) MQ_PAIR_LAUNCH(5, false, 2);
+    else if (hyp == 1) MQ_PAIR_LAUNCH(5, false, 1);
+    else MQ_PAIR_LAUNCH(5, false, 0);
   } else {
-    if (g5) hipLaunchKernelGGL((gru_fwd_pair_kernel<5, false, 0>), g, b, 0, s, d, rp, P0, P1, L, w);
-    else hipLaunchKernelGGL((gru_fwd_pair_kernel<FGATHER, false, 0>), g, b, 0, s, d, rp, P0, P1, L, w);
+    if (hyp == 2) MQ_PAIR_LAUNCH(FGATHER, false, 2);
+    else if (hyp == 1) MQ_PAIR_LAUNCH(FGATHER, false, 1);
+    else MQ_PAIR_LAUNCH(FGATHER, false, 0);
   }
+#undef MQ_PAIR_LAUNCH
 }
 
 }  // namespace mq

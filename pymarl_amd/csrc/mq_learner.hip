@@ -115,7 +115,8 @@ struct mq_handle {
   int dwh_in_bwd = getenv("MQ_DWH_IN_BWD") ? atoi(getenv("MQ_DWH_IN_BWD")) : -1;
   // the row-pair forward (gru_fwd_pair.hpp: both nets of a row in one workgroup, one per CU) when the rows fit one
   // wave of workgroups; MQ_FWD_PAIR=0 keeps the one-row-net kernel, =1 forces the pair (A/B switches)
-  int fwd_pair = getenv("MQ_FWD_PAIR") ? atoi(getenv("MQ_FWD_PAIR")) : 0;   // TEMP default off until GPU-verified
+  int fwd_pair = getenv("MQ_FWD_PAIR") ? atoi(getenv("MQ_FWD_PAIR")) : -1;
+  bool pair_hyp_epi = getenv("MQ_PAIR_HYP_EPI") != nullptr;
   // MQ_MIX_GENERIC=1: mix_kernel<false> where mix_kernel<true> (staged selection rows) would run (A/B switch)
   bool mix_generic = getenv("MQ_MIX_GENERIC") != nullptr;
   int num_cu = 0;
@@ -488,9 +489,13 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
                    hyf_ok(d.S, d.E, d.NH, d.M);
       if (hyp_in_fwd) plan.hyper = MQ_HYP_WS;
       const char* stamp_path = getenv("MQ_PAIR_STAMP");   // diagnostic: step stamps of the first 8 workgroups
-      launch_fwd_pair(s, d, rp, (const float*)h->on, (const float*)h->tg, L, w, hyp_in_fwd, stamp_path != nullptr);
-      if (stamp_path && FCH * d.O <= 256 * 5) {
-        std::vector<uint32_t> st((size_t)8 * 3 * d.Tp);
+      // on waves 4 / 5 inside the kernel when every hypernet block has a workgroup, else as its epilogue
+      // (MQ_PAIR_HYP_EPI forces the epilogue)
+      const int pair_hyp = !hyp_in_fwd ? 0 : (2 * ((d.M + 31) / 32) <= d.R && !h->pair_hyp_epi) ? 2 : 1;
+      launch_fwd_pair(s, d, rp, (const float*)h->on, (const float*)h->tg, L, w, pair_hyp,
+                      stamp_path != nullptr && d.Tp <= 512);
+      if (stamp_path && FCH * d.O <= 256 * 5 && d.Tp <= 512) {
+        std::vector<uint32_t> st((size_t)8 * PST);
         MQ_HIP(hipMemcpyAsync(st.data(), w.slab_rnn, st.size() * 4, hipMemcpyDeviceToHost, s));
         MQ_HIP(hipStreamSynchronize(s));
         if (FILE* f = fopen(stamp_path, "ab")) { fwrite(st.data(), 4, st.size(), f); fclose(f); }

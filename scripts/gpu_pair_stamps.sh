@@ -1,8 +1,7 @@
 #!/bin/bash
-# Step stamps of the row-pair forward at cfg2 (split and shared roles).
+# Stamps of the row-pair forward at cfg2 (scripts/pair_stamps.py).
 set -o pipefail
-O=gpurun_out; mkdir -p $O
-for v in 1 0; do rm -f $O/stamps_$v.bin
-  MQ_PAIR_SPLIT=$v MQ_PAIR_STAMP=$O/stamps_$v.bin timeout -k 10 200 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2> $O/stamps_$v.err || exit 1
-  echo "split=$v"; python scripts/pair_stamps.py $O/stamps_$v.bin 121 || exit 1
-done
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; mkdir -p $O; T=${1:-r05q}
+rm -f $O/${T}_stamps.bin
+MQ_PAIR_STAMP=$O/${T}_stamps.bin timeout -k 10 200 python bench.py --steps 3 --warmup 2 --no-cpu-baseline > /dev/null 2> $O/${T}_stamps.err || exit 1
+python scripts/pair_stamps.py $O/${T}_stamps.bin 121

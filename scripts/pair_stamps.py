@@ -1,19 +1,27 @@
-"""Decode the row-pair forward's stamps (MQ_PAIR_STAMP=<file>, gru_fwd_pair.hpp STAMP) of the last train(): the
-recurrence's cycles per step inside a chunk, across a chunk boundary, and how early or late the producers reach each
-chunk barrier relative to the recurrence. Usage: python scripts/pair_stamps.py <file> <Tp>"""
+"""Decode the row-pair forward's stamps (MQ_PAIR_STAMP=<file>, gru_fwd_pair.hpp STAMP) of the last train(), cycles
+(s_memtime ticks) from kernel entry: prologue, recurrence loop, epilogue; per-step cost inside a chunk and across a
+chunk boundary; producers' slack at each chunk barrier. Usage: python scripts/pair_stamps.py <file> <Tp>"""
 import sys
 import numpy as np
 
+PST = 16 + 2 * 512
 path, Tp = sys.argv[1], int(sys.argv[2])
-a = np.fromfile(path, dtype=np.uint32)
-a = a[-8 * 3 * Tp:].reshape(8, 3, Tp).astype(np.int64)   # [block][step end, rec chunk arrival, prod chunk arrival][t]
-end, arr_r, arr_p = a[:, 0], a[:, 1], a[:, 2]
-per = np.diff(end, axis=1)                                # cycles of step t (t >= 1)
+a = np.fromfile(path, dtype=np.uint32)[-8 * PST:].reshape(8, PST).astype(np.int64)
+rel = (a - a[:, :1]) % (1 << 32)
+entry, lstart, lend, pro, kend = (rel[:, i] for i in range(5))
+steps = rel[:, 16:16 + Tp]
+print("per block (mean of 8): recurrence loop starts at %.0f, producers' prologue done at %.0f, loop ends at %.0f,"
+      " kernel ends at %.0f cycles" % (lstart.mean(), pro.mean(), lend.mean(), kend.mean()))
+per = np.diff(steps, axis=1)
 t = np.arange(1, Tp)
-inside, first = per[:, (t % 16) != 0], per[:, (t % 16) == 0]
+ins = (t % 16) != 0
+print("producers: loads issued %.0f, landed %.0f, X1(0..1) %.0f, GI(0) %.0f; recurrence W_hh landed %.0f" %
+      tuple(rel[:, i].mean() for i in (5, 6, 7, 8, 9)))
+print("hypernet waves (HYP=2): tiles done in the S3/S4/S5/chunk-0 intervals %s, exit %.0f" % ([round(rel[:, 11 + i].mean()) for i in range(4)], rel[:, 15].mean()))
+print("step cycles inside a chunk: mean %.0f, median %.0f; first step of a chunk: mean %.0f; step 0 ends %.0f after "
+      "the loop start" % (per[:, ins].mean(), np.median(per[:, ins]), per[:, ~ins].mean(),
+                          (steps[:, 0] - lstart).mean()))
 last = np.arange(15, Tp, 16)
-print("steps inside a chunk: mean %.0f, median %.0f cycles; first step of a chunk: mean %.0f" %
-      (inside.mean(), np.median(inside), first.mean()))
-print("whole T loop %.0f cycles (%d steps)" % ((end[:, -1] - end[:, 0]).mean(), Tp))
-print("producer arrival - recurrence arrival at each chunk barrier (cycles, + = producers late):")
-print(" ", np.round((arr_p[:, last] - arr_r[:, last]).mean(0)).astype(int).tolist())
+arr = rel[:, 16 + 512 + last]
+print("producers' chunk-barrier arrival - recurrence's chunk end (cycles, + = producers late):",
+      np.round((arr - steps[:, last]).mean(0)).astype(int).tolist())

@@ -499,14 +499,19 @@ def test_hyper_in_forward_grid_bitwise(cases, name, monkeypatch):
 
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg1_qmix", "tiny_qmix_full", "cfg2_qmix_ragged"])
 def test_pair_hyper_epilogue_bitwise(cases, name, monkeypatch):
-    """The QMIX hypernet as the row-pair forward's epilogue (the default with the pair kernel) equals hyper_ws_kernel
-    launched after the forward (MQ_HYP_IN_FWD=0) bitwise: parameters, gradients, square_avg and stats over up to
-    four steps, ragged M included."""
+    """The QMIX hypernet inside the row-pair forward — on waves 4 / 5 during the T loop (the default when every
+    hypernet block has a workgroup) or as the kernel's epilogue (MQ_PAIR_HYP_EPI=1, and the default otherwise) —
+    equals hyper_ws_kernel launched after the forward (MQ_HYP_IN_FWD=0) bitwise: parameters, gradients, square_avg
+    and stats over up to four steps, ragged M included."""
     from tests.gpu_helpers import build, flat_grads, flat_params
     case = get_case(cases, name)
     outs = []
     monkeypatch.setenv("MQ_FWD_PAIR", "1")
-    for inf in (None, "0"):
+    for inf, epi in ((None, False), (None, True), ("0", False)):
+        if epi:
+            monkeypatch.setenv("MQ_PAIR_HYP_EPI", "1")
+        else:
+            monkeypatch.delenv("MQ_PAIR_HYP_EPI", raising=False)
         if inf is None:
             monkeypatch.delenv("MQ_HYP_IN_FWD", raising=False)
         else:
@@ -519,10 +524,11 @@ def test_pair_hyper_epilogue_bitwise(cases, name, monkeypatch):
         th.cuda.synchronize()
         assert learner.last_plan()["hyper"] == "ws" and learner.last_plan()["fused_fwd"] == 2
         outs.append((flat_params(learner), flat_grads(learner), learner._sq.cpu().numpy(), learner.last_stats()))
-    assert np.array_equal(outs[0][0], outs[1][0])
-    assert np.array_equal(outs[0][1], outs[1][1])
-    assert np.array_equal(outs[0][2], outs[1][2])
-    assert outs[0][3] == outs[1][3]
+    for o in outs[1:]:
+        assert np.array_equal(outs[0][0], o[0])
+        assert np.array_equal(outs[0][1], o[1])
+        assert np.array_equal(outs[0][2], o[2])
+        assert outs[0][3] == o[3]
 
 
 @pytest.mark.parametrize("name", ["cfg3_vdn", "cfg3_qmix", "cfg3_vdn_b128"])
