@@ -31,7 +31,7 @@ extern "C" {
 
 enum { MQ_MIXER_NONE = 0, MQ_MIXER_VDN = 1, MQ_MIXER_QMIX = 2 };
 enum { MQ_OK = 0, MQ_ERR_ARG = 1, MQ_ERR_HIP = 2, MQ_ERR_STATE = 3 };
-enum { MQ_NSUMS = 8 };   /* tail of the gradient buffer: sum (td*m)^2, sum m, sum |td*m|, sum Q_tot*m, sum y*m */
+enum { MQ_NSUMS = 8 };   /* tail of the gradient buffer: sum (td*m)^2 (Huber: sum huber(td*m)), sum m, sum |td*m|, sum Q_tot*m, sum y*m */
 enum { MQ_NSTATS = 8 };  /* loss, grad_norm, td_error_abs, q_taken_mean, target_mean, mask_sum */
 
 /* Parameter tensors, in the reference's parameters()/state_dict order: RNNAgent (rnn_agent.py:19-21) then
@@ -51,6 +51,8 @@ typedef struct mq_config {
   float gamma, lr, optim_alpha, optim_eps, grad_norm_clip;
   int32_t max_batch;         /* most episodes one call may train on (workspace bound) */
   int32_t max_seq;           /* most stored steps per episode (episode_limit + 1) */
+  float huber_delta;         /* TD loss: 0 = masked L2 (q_learner.py:96-97, default); > 0 = masked Huber with this
+                                delta, an opt-in the reference lacks (not pinned by its goldens) */
 } mq_config;
 
 /* A batch of episodes as the learner reads it: the replay storage (reference scheme dtypes, episode-major

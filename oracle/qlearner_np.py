@@ -273,7 +273,12 @@ class OracleQLearner:
         m = np.broadcast_to(mask, td.shape).astype(F32)
         mtd = td * m
         msum = F32(m.sum())
-        loss = F32((mtd * mtd).sum()) / msum
+        hd = F32(c.get("huber_delta", 0.0))
+        if hd > 0:   # opt-in masked Huber (no reference counterpart: parity unpinned; L2 below is q_learner.py:96-97)
+            ax = np.abs(mtd)
+            loss = F32(np.where(ax <= hd, F32(0.5) * mtd * mtd, hd * (ax - F32(0.5) * hd)).astype(F32).sum()) / msum
+        else:
+            loss = F32((mtd * mtd).sum()) / msum
         return dict(mac_out=mac_out, target_mac_out=tmo, cur_max_actions=cur_max, chosen=chosen,
                     target_max=target_max, q_tot=q_tot, target_q_tot=tq_tot, targets=targets, td=td, mask=m,
                     mask_sum=msum, loss=float(loss), acache=acache, mcache=mcache, actions=actions)
@@ -284,7 +289,11 @@ class OracleQLearner:
         fw = fw or self.forward(batch, keep_cache=True, cur_max_override=cur_max_override,
                                 relu_override=relu_override)
         td, m, msum = fw["td"], fw["mask"], fw["mask_sum"]
-        dq_tot = ((F32(2.0) * (td * m)) * (F32(1.0) / msum)) * m            # d/dQ_tot of sum((td*m)^2)/sum(m)
+        hd = F32(c.get("huber_delta", 0.0))
+        if hd > 0:   # d/dQ_tot of sum(huber(td*m))/sum(m)
+            dq_tot = (np.clip(td * m, -hd, hd) * m * (F32(1.0) / msum)).astype(F32)
+        else:
+            dq_tot = ((F32(2.0) * (td * m)) * (F32(1.0) / msum)) * m            # d/dQ_tot of sum((td*m)^2)/sum(m)
         B, T = td.shape[:2]
         n = c["n_agents"]
         mg = OrderedDict()

@@ -52,7 +52,7 @@ class MQConfig(ctypes.Structure):
         ("mixer", ctypes.c_int32), ("double_q", ctypes.c_int32), ("obs_last_action", ctypes.c_int32),
         ("obs_agent_id", ctypes.c_int32), ("gamma", ctypes.c_float), ("lr", ctypes.c_float),
         ("optim_alpha", ctypes.c_float), ("optim_eps", ctypes.c_float), ("grad_norm_clip", ctypes.c_float),
-        ("max_batch", ctypes.c_int32), ("max_seq", ctypes.c_int32),
+        ("max_batch", ctypes.c_int32), ("max_seq", ctypes.c_int32), ("huber_delta", ctypes.c_float),
     ]
 
 

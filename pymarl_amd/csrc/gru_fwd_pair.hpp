@@ -63,25 +63,31 @@ MQ_DEV uint32_t stamp_now() {
 // in LDS, the B fragments come straight from the parameters (one tile ahead, in registers). Operand maps, K order and
 // bias add are hyper_ws_kernel's: HYP and S0 are bitwise its outputs.
 constexpr int HT_SP = 4 * 48 + 4;   // row pitch of the staged states (K padded to 192, zeros)
-// tiles a wave has finished by the end of the interval that barrier i (0 = S1) opens: none before S3 (W_ih staging),
-// then 1, 2 and 2 in the prologue intervals, the rest spread over the chunks
-MQ_DEV int hyp_tiles_by(int i, int cnt, int nchunks) {
-  constexpr int kPro[4] = {0, 1, 3, 5};
+// Tiles a wave has finished by the end of the interval that barrier i (0 = S1) opens, from the schedule `hs`: nibbles
+// 0..3 the cumulative counts after the S3, S4, S5 and chunk-0 intervals (the prologue's slack: the recurrences wait
+// for the producers' first chunks there), nibble 4 the tiles left for the interval after the last chunk barrier
+// (beside the producers' last fc2 and records); the rest spread evenly over chunks 1 .. cl, where every MFMA delays
+// the recurrence wave sharing the SIMD by about its own issue time (stamps, round 5).
+MQ_DEV int hyp_tiles_by(int i, int cnt, int nbar, int hs) {
   if (i < 2) return 0;
-  if (i < 6) return min(cnt, kPro[i - 2]);
-  const int rem = max(cnt - kPro[3], 0), c = i - 5;   // chunk c - 1 done
-  return min(cnt, kPro[3] + (rem * c + nchunks - 1) / nchunks);
+  if (i < 6) return min(cnt, (hs >> (4 * (i - 2))) & 15);
+  if (i >= nbar - 1) return cnt;
+  const int c5 = min(cnt, (hs >> 12) & 15), rem = max(cnt - c5 - ((hs >> 16) & 15), 0);
+  const int nl = nbar - 7;   // chunks 1 .. cl (i = 6 .. nbar - 2)
+  return min(cnt, c5 + (rem * (i - 5) + nl - 1) / nl);
 }
+constexpr int kHypSched = 0x08642;
 template <bool STAMP, class StageWih>
 MQ_DEV void hyper_waves(const Dims& d, const Rep& rp, const float* __restrict__ P0, const float* __restrict__ P1,
-                        const Lay& L, const Work& w, float* hst, uint32_t* stl, int nbar, StageWih stage_wih) {
+                        const Lay& L, const Work& w, float* hst, uint32_t* stl, int nbar, int hsched,
+                        StageWih stage_wih) {
   const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
   const int hw = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) - 4;
   const int hb = blockIdx.x, S = d.S, NH = d.NH, E = d.E, nE = d.n * d.E;
   const bool act = hb < 2 * ((d.M + 31) / 32);   // the host launches HYP = 2 only when every block has a row
   const int z = hb & 1, m0 = (hb >> 1) * 32;
   const float* __restrict__ P = z ? P1 : P0;
-  const int NT = NH / 16, cnt = act ? (NT - hw + 1) / 2 : 0, nchunks = nbar - 6;
+  const int NT = NH / 16, cnt = act ? (NT - hw + 1) / 2 : 0;
   // states: wave hw gathers rows 16 hw .. 16 hw + 15 (lanes: columns l, l + 64, l + 128) and stages them
   if (act) {
     float vs[16][3];
@@ -112,16 +118,17 @@ MQ_DEV void hyper_waves(const Dims& d, const Rep& rp, const float* __restrict__ 
       (void*)(w.HYP + (int64_t)z * d.M * NH), (short)0, (int)((int64_t)d.M * NH * sizeof(float)), 0x00020000);
   f32x4 ba[12], bb[12];
   float bja = 0.0f, bjb = 0.0f;
-  auto fetch = [&](int k, f32x4 (&bf)[12], float& bj) {   // B fragments of local tile k: row j, columns 48 g ..
-    const int j = 16 * (hw + 2 * k) + c16;
-    const HypSeg sg = hyp_seg(L, nE, E, j);
-    const int base = (int)(sg.w + (int64_t)sg.row * S) * 4 + 192 * g;
+  auto fetch = [&](int k, f32x4 (&bf)[12], float& bj) {   // B fragments of local tile k: row j0 + c16, columns 48 g ..
+    const HypSeg sg = hyp_seg(L, nE, E, 16 * (hw + 2 * k));   // wave-uniform: a 16-row tile never straddles segments
+    const int row = sg.row + c16;
+    const int base = (int)(sg.w + (int64_t)row * S) * 4 + 192 * g;
 #pragma unroll
     for (int mm = 0; mm < 12; ++mm)
       bf[mm] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(prs, base + 16 * mm, 0, 0));
-    bj = P[sg.b + sg.row];
+    bj = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(prs, (int)(sg.b + row) * 4, 0, 0));
+    __builtin_amdgcn_sched_barrier(0);   // the loads stay ahead of the MFMAs that follow
   };
-  const float* a0 = hst + c16 * HT_SP + 48 * g;
+  const float* a0 = hst + c16 * HT_SP + 48 * g;   // A fragments: states rows c16 and 16 + c16, columns 48 g ..
   const float* a1 = a0 + 16 * HT_SP;
   auto tile = [&](int k, const f32x4 (&bf)[12], float bj) {
     f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
@@ -146,15 +153,19 @@ MQ_DEV void hyper_waves(const Dims& d, const Rep& rp, const float* __restrict__ 
   int done = 0;
   for (int i = 2; i < nbar; ++i) {
     lds_barrier();   // barrier i (S3 .. the last chunk's)
-    const int upto = hyp_tiles_by(i, cnt, nchunks);
-    while (done < upto) {   // wave-uniform
-      if (done & 1) {
-        if (done + 1 < cnt) fetch(done + 1, ba, bja);
-        tile(done, bb, bjb);
-      } else {
-        if (done + 1 < cnt) fetch(done + 1, bb, bjb);
-        tile(done, ba, bja);
-      }
+    // tiles go in pairs (even k on set a, odd on set b) so both register sets keep fixed roles, and every prefetch
+    // is unconditional (past the last tile a harmless repeat): with a set chosen at run time, or a prefetch behind a
+    // branch, the compiler joined the sets with copies and waited for the loads just issued (ISA, round 5)
+    const int upto = i < nbar - 1 ? hyp_tiles_by(i, cnt, nbar, hsched) & ~1 : cnt;
+    while (done + 1 < upto) {   // wave-uniform
+      fetch(min(done + 1, cnt - 1), bb, bjb);
+      tile(done, ba, bja);
+      fetch(min(done + 2, cnt - 1), ba, bja);
+      tile(done + 1, bb, bjb);
+      done += 2;
+    }
+    if (done < upto) {   // the odd last tile (final interval only)
+      tile(done, ba, bja);
       ++done;
     }
     if constexpr (STAMP) {
@@ -166,7 +177,8 @@ MQ_DEV void hyper_waves(const Dims& d, const Rep& rp, const float* __restrict__ 
 
 template <int NG, bool STAMP, int HYP = 0>
 MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0, const float* __restrict__ P1,
-                      const Lay& L, const Work& w, PairLds& S, uint32_t* stl, float* hst = nullptr) {
+                      const Lay& L, const Work& w, PairLds& S, uint32_t* stl, float* hst = nullptr,
+                      int hsched = kHypSched) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int R = d.R, Tp = d.Tp, I = d.I, O = d.O, A = d.A, n = d.n;
@@ -216,7 +228,7 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
   if (!producer) {
     if (wv >= 2) {   // waves 4, 5 (the recurrence SIMDs' second slots)
       if constexpr (HYP == 2) {
-        hyper_waves<STAMP>(d, rp, P0, P1, L, w, hst, stl, kPrologueBarriers + cl + 1,
+        hyper_waves<STAMP>(d, rp, P0, P1, L, w, hst, stl, kPrologueBarriers + cl + 1, hsched,
                            [&]() { stage_rows((int)L.o[MQ_P_RNN_W_IH], 384, 64 * (wv - 4) + lane); });
         return;
       }
@@ -524,7 +536,8 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
 // waves 4 / 5 during the prologue and T loop (hyper_waves above), one block per workgroup.
 template <int NG, bool STAMP = false, int HYP = 0>
 __global__ __launch_bounds__(512, 1) void gru_fwd_pair_kernel(Dims d, Rep rp, const float* __restrict__ P0,
-                                                              const float* __restrict__ P1, Lay L, Work w) {
+                                                              const float* __restrict__ P1, Lay L, Work w,
+                                                              int hsched) {
   __shared__ PairLds S;
   static_assert(sizeof(PairLds) >= hyf_floats() * sizeof(float), "the hypernet epilogue reuses the forward's LDS");
   __shared__ uint32_t stl[STAMP ? PST : 1];
@@ -533,7 +546,7 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_pair_kernel(Dims d, Rep rp, co
     const uint32_t t0 = stamp_now();
     if (threadIdx.x == 0) stl[0] = t0;
   }
-  pair_body<NG, STAMP, HYP>(d, rp, P0, P1, L, w, S, stl, hst);
+  pair_body<NG, STAMP, HYP>(d, rp, P0, P1, L, w, S, stl, hst, hsched);
   if constexpr (HYP == 1) {
     const int nhb = 2 * ((d.M + 31) / 32);
     for (int hb = blockIdx.x; hb < nhb; hb += gridDim.x) {
@@ -553,10 +566,11 @@ __global__ __launch_bounds__(512, 1) void gru_fwd_pair_kernel(Dims d, Rep rp, co
 
 // Host: the row-pair forward, grid R, with the smallest gather-slot instantiation that covers O.
 inline void launch_fwd_pair(hipStream_t s, const Dims& d, const Rep& rp, const float* P0, const float* P1,
-                            const Lay& L, const Work& w, int hyp, bool stamp = false) {
+                            const Lay& L, const Work& w, int hyp, bool stamp = false,
+                            int hsched = kHypSched) {
   const dim3 g(d.R), b(512);
   const bool g5 = FCH * d.O <= 256 * 5;
-#define MQ_PAIR_LAUNCH(NG, ST, HY) hipLaunchKernelGGL((gru_fwd_pair_kernel<NG, ST, HY>), g, b, 0, s, d, rp, P0, P1, L, w)
+#define MQ_PAIR_LAUNCH(NG, ST, HY) hipLaunchKernelGGL((gru_fwd_pair_kernel<NG, ST, HY>), g, b, 0, s, d, rp, P0, P1, L, w, hsched)
   if (stamp) {
     if (hyp == 2) MQ_PAIR_LAUNCH(5, true, 2);
     else if (hyp == 1) MQ_PAIR_LAUNCH(5, true, 1);

@@ -14,9 +14,24 @@ struct Dims {
   int t_stride;              // storage max_seq_length
   int last_action, agent_id, mixer, double_q;
   float gamma;
+  float huber;                      // TD loss: 0 = masked L2 (the reference), > 0 = Huber delta (opt-in)
   FastDiv dR, dN, dB, dO, dI, dS;   // fast division by R, n, B, obs / agent-input / state widths
   MQ_DEV int64_t RT() const { return (int64_t)Tp * R; }
 };
+
+// The masked TD loss term of one transition and its derivative d/dQ_tot (before the 1 / mask_sum scale).
+// delta == 0: L2, (td m)^2 (q_learner.py:96-97, the reference's loss and the default). delta > 0: Huber, an opt-in
+// the reference lacks (north_star names it): 0.5 x^2 for |x| <= delta, delta (|x| - delta / 2) beyond, x = td m.
+MQ_DEV float td_loss(float mtd, float delta) {
+  if (delta > 0.0f) {
+    const float ax = fabsf(mtd);
+    return ax <= delta ? 0.5f * mtd * mtd : delta * (ax - 0.5f * delta);
+  }
+  return mtd * mtd;
+}
+MQ_DEV float td_dy(float mtd, float mask, float delta) {
+  return delta > 0.0f ? fminf(fmaxf(mtd, -delta), delta) * mask : (2.0f * mtd) * mask;
+}
 
 // Borrowed replay storage (reference scheme dtypes), episode-major, plus the sampled episode ids.
 struct Rep {

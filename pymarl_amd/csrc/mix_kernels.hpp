@@ -188,8 +188,8 @@ __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* _
     const float target = rew + gamma * (1.0f - term) * yt;   // q_learner.py:86
     const float td = y - target;
     const float mtd = td * mask;
-    l2 = mtd * mtd; msk = mask; abs_ = fabsf(mtd); qs = y * mask; tg = target * mask;
-    const float dy = (2.0f * mtd) * mask;                     // d sum (td*m)^2 / d Q_tot
+    l2 = td_loss(mtd, d.huber); msk = mask; abs_ = fabsf(mtd); qs = y * mask; tg = target * mask;
+    const float dy = td_dy(mtd, mask, d.huber);   // d sum loss(td*m) / d Q_tot
     // ---- QMIX backward (lanes e < E)
     float dpre = 0.0f;
     if (valid && lane < E) {
@@ -237,12 +237,12 @@ __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* _
     const float target = rew + gamma * (1.0f - term) * yt;
     const float td = y - target;
     const float mtd = td * mask;
-    const float dy = (2.0f * mtd) * mask;
+    const float dy = td_dy(mtd, mask, d.huber);
     if (d.mixer == MQ_MIXER_VDN) {
-      l2 = mtd * mtd; msk = mask; abs_ = fabsf(mtd); qs = y * mask; tg = target * mask;
+      l2 = td_loss(mtd, d.huber); msk = mask; abs_ = fabsf(mtd); qs = y * mask; tg = target * mask;
     } else {
       const bool on = lane < n;
-      l2 = wave_sum(on ? mtd * mtd : 0.0f);
+      l2 = wave_sum(on ? td_loss(mtd, d.huber) : 0.0f);
       msk = wave_sum(on ? mask : 0.0f);
       abs_ = wave_sum(on ? fabsf(mtd) : 0.0f);
       qs = wave_sum(on ? y * mask : 0.0f);
@@ -414,8 +414,8 @@ MQ_DEV void mix_fast_row(const Dims& d, const Rep& rp, const float* __restrict__
     const float target = rew + gamma * (1.0f - term) * yt;   // q_learner.py:86
     const float td = y - target;
     const float mtd = td * mask;
-    l2 = mtd * mtd; msk = mask; abs_ = fabsf(mtd); qs = y * mask; tg = target * mask;
-    const float dy = (2.0f * mtd) * mask;
+    l2 = td_loss(mtd, d.huber); msk = mask; abs_ = fabsf(mtd); qs = y * mask; tg = target * mask;
+    const float dy = td_dy(mtd, mask, d.huber);
     float dpre = 0.0f;
     if (e_lane) {
       const float wf = fabsf(xon[0]);
@@ -450,12 +450,12 @@ MQ_DEV void mix_fast_row(const Dims& d, const Rep& rp, const float* __restrict__
     const float target = rew + gamma * (1.0f - term) * yt;
     const float td = y - target;
     const float mtd = td * mask;
-    const float dy = (2.0f * mtd) * mask;
+    const float dy = td_dy(mtd, mask, d.huber);
     if (d.mixer == MQ_MIXER_VDN) {
-      l2 = mtd * mtd; msk = mask; abs_ = fabsf(mtd); qs = y * mask; tg = target * mask;
+      l2 = td_loss(mtd, d.huber); msk = mask; abs_ = fabsf(mtd); qs = y * mask; tg = target * mask;
     } else {
       const bool on = lane < n;
-      l2 = wave_sum(on ? mtd * mtd : 0.0f);
+      l2 = wave_sum(on ? td_loss(mtd, d.huber) : 0.0f);
       msk = wave_sum(on ? mask : 0.0f);
       abs_ = wave_sum(on ? fabsf(mtd) : 0.0f);
       qs = wave_sum(on ? y * mask : 0.0f);

@@ -117,6 +117,8 @@ struct mq_handle {
   // wave of workgroups; MQ_FWD_PAIR=0 keeps the one-row-net kernel, =1 forces the pair (A/B switches)
   int fwd_pair = getenv("MQ_FWD_PAIR") ? atoi(getenv("MQ_FWD_PAIR")) : -1;
   bool pair_hyp_epi = getenv("MQ_PAIR_HYP_EPI") != nullptr;
+  // MQ_HYP_SCHED=<hex>: the in-forward hypernet's tile schedule (gru_fwd_pair.hpp hyp_tiles_by; tuning switch)
+  int hyp_sched = getenv("MQ_HYP_SCHED") ? (int)strtol(getenv("MQ_HYP_SCHED"), nullptr, 16) : kHypSched;
   // MQ_MIX_GENERIC=1: mix_kernel<false> where mix_kernel<true> (staged selection rows) would run (A/B switch)
   bool mix_generic = getenv("MQ_MIX_GENERIC") != nullptr;
   int num_cu = 0;
@@ -163,6 +165,7 @@ Dims make_dims(const mq_handle* h, const mq_replay* b) {
   d.t_stride = b->t_stride;
   d.last_action = c.obs_last_action; d.agent_id = c.obs_agent_id; d.mixer = c.mixer; d.double_q = c.double_q;
   d.gamma = c.gamma;
+  d.huber = c.huber_delta;
   d.dR = make_fastdiv((uint32_t)d.R);
   d.dN = make_fastdiv((uint32_t)d.n);
   d.dB = make_fastdiv((uint32_t)d.B);
@@ -324,6 +327,7 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
   if (c.mixer == MQ_MIXER_QMIX && (c.mixing_embed_dim < 1 || c.mixing_embed_dim > 64))
     return set_err(MQ_ERR_ARG, "mixing_embed_dim must be in [1, 64]");
   if (c.max_batch < 1 || c.max_seq < 2) return set_err(MQ_ERR_ARG, "max_batch >= 1 and max_seq >= 2 required");
+  if (!(c.huber_delta >= 0.0f)) return set_err(MQ_ERR_ARG, "huber_delta must be >= 0 (0: the reference's L2 loss)");
 
   mq_handle* h = new mq_handle();
   h->cfg = c;
@@ -493,7 +497,7 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
       // (MQ_PAIR_HYP_EPI forces the epilogue)
       const int pair_hyp = !hyp_in_fwd ? 0 : (2 * ((d.M + 31) / 32) <= d.R && !h->pair_hyp_epi) ? 2 : 1;
       launch_fwd_pair(s, d, rp, (const float*)h->on, (const float*)h->tg, L, w, pair_hyp,
-                      stamp_path != nullptr && d.Tp <= 512);
+                      stamp_path != nullptr && d.Tp <= 512, h->hyp_sched);
       if (stamp_path && FCH * d.O <= 256 * 5 && d.Tp <= 512) {
         std::vector<uint32_t> st((size_t)8 * PST);
         MQ_HIP(hipMemcpyAsync(st.data(), w.slab_rnn, st.size() * 4, hipMemcpyDeviceToHost, s));

@@ -62,6 +62,9 @@ def make_config(args, mixer, input_dim=None, max_batch=1, max_seq=2):
     cfg.grad_norm_clip = getattr(args, "grad_norm_clip", 10.0)
     cfg.max_batch = int(max_batch)
     cfg.max_seq = int(max_seq)
+    # opt-in masked Huber TD loss (north_star; the reference has L2 only, q_learner.py:96-97): td_loss: huber,
+    # huber_delta (default 1.0); anything else keeps L2
+    cfg.huber_delta = float(getattr(args, "huber_delta", 1.0)) if getattr(args, "td_loss", "l2") == "huber" else 0.0
     return cfg
 
 

@@ -35,8 +35,8 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
 #include <stddef.h>
 #include "mc_coma.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu\\n", sizeof(mq_config), offsetof(mq_config, gamma), offsetof(mq_config, max_seq),
-         sizeof(mq_replay), offsetof(mq_replay, batch_size));
+  printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(mq_config), offsetof(mq_config, gamma), offsetof(mq_config, max_seq),
+         offsetof(mq_config, huber_delta), sizeof(mq_replay), offsetof(mq_replay, batch_size));
   printf("%d %d\\n", MQ_P_COUNT, MQ_NSUMS);
   printf("%zu %zu %zu %d %d %d\\n", sizeof(mc_config), offsetof(mc_config, gamma), offsetof(mc_config, max_seq),
          MC_P_COUNT, MC_NTAIL, MC_NSTATS);
@@ -49,6 +49,7 @@ int main(void) {
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
     c = [int(x) for x in out]
     py = [ctypes.sizeof(_lib.MQConfig), _lib.MQConfig.gamma.offset, _lib.MQConfig.max_seq.offset,
+          _lib.MQConfig.huber_delta.offset,
           ctypes.sizeof(_lib.MQReplay), _lib.MQReplay.batch_size.offset, _lib.P_COUNT, _lib.NSUMS,
           ctypes.sizeof(_lib.MCConfig), _lib.MCConfig.gamma.offset, _lib.MCConfig.max_seq.offset, _lib.MC_P_COUNT,
           _lib.MC_NTAIL, _lib.MC_NSTATS, ctypes.sizeof(_lib.MQPlan), _lib.MQPlan.inline_ids.offset,

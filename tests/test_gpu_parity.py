@@ -390,8 +390,9 @@ def sample_like_reference(buf, case, args, flow):
     return batch
 
 
-def run_teacher_forced(case, steps, unfused, monkeypatch, flow="view"):
-    """Every step from the oracle's state; decisions, stats, gradients and the RMSprop step checked (see module doc)."""
+def run_teacher_forced(case, steps, unfused, monkeypatch, flow="view", huber=0.0):
+    """Every step from the oracle's state; decisions, stats, gradients and the RMSprop step checked (see module doc).
+    huber > 0: the opt-in masked Huber TD loss with that delta on both sides (no reference golden for it)."""
     from oracle.qlearner_np import OracleQLearner
     from tests.gpu_helpers import build, flat_grads, flat_params, rel
     name = case.name
@@ -400,11 +401,13 @@ def run_teacher_forced(case, steps, unfused, monkeypatch, flow="view"):
             monkeypatch.setenv(k, "1")
         else:
             monkeypatch.delenv(k, raising=False)
-    args, buf, mac, learner, logger = build(case, buffer_device="cpu" if flow == "cpu_to" else None)
-    o = OracleQLearner(case.agent_params, case.mixer_params, case.cfg())
+    over = {"td_loss": "huber", "huber_delta": huber} if huber else {}
+    args, buf, mac, learner, logger = build(case, buffer_device="cpu" if flow == "cpu_to" else None, **over)
+    o = OracleQLearner(case.agent_params, case.mixer_params, dict(case.cfg(), huber_delta=huber))
     np.random.seed(case.sampler_seed)
     rec = []
     strided = truncated = 0
+    regimes = set()
     for k in range(steps):
         batch = sample_like_reference(buf, case, args, flow)
         if flow == "dense_slice":
@@ -418,7 +421,11 @@ def run_teacher_forced(case, steps, unfused, monkeypatch, flow="view"):
         st = learner.last_stats()
         if flow != "view":
             assert learner.last_plan()["inline_ids"] == 0, "a dense batch must not take the episode-id path"
-        if k == 0 and "stat_loss" in case.z:   # the same starting state as the reference golden run: its stats
+        if huber:
+            ax = np.abs(fw["td"] * fw["mask"])[fw["mask"] > 0]
+            regimes |= {"quadratic"} if (ax <= huber).any() else set()
+            regimes |= {"linear"} if (ax > huber).any() else set()
+        if k == 0 and "stat_loss" in case.z and not huber:   # the reference golden run's start: its stats
             for s_ in STATS:
                 ref = float(case.z["stat_" + s_][0])
                 assert abs(st[s_] - ref) <= 1e-4 * abs(ref) + 1e-6, (name, flow, s_, st[s_], ref)
@@ -445,13 +452,25 @@ def run_teacher_forced(case, steps, unfused, monkeypatch, flow="view"):
         assert rel(learner._sq.cpu().numpy(), sq_exp) < 1e-5, (name, k)
         assert rel(flat_params(learner), p_exp) < 1e-6, (name, k)
         assert np.abs(flat_params(learner) - o.flat("params")).max() <= 20 * 5e-4, (name, k)
+    if huber:
+        assert regimes == {"quadratic", "linear"}, (name, regimes)   # both branches of the loss exercised
     if flow == "dense_slice":   # every truncated batch is read in place with t_stride = T + 1 > t_len
         assert strided == truncated, (strided, truncated)
         assert case.name != "cfg1_qmix" or strided == steps
     tag = "_tiles" if os.environ.get("MQ_ROW_TILES") == "1" else ""
-    write_record("teacher" + ("_unfused" if unfused else "") + tag + ("" if flow == "view" else "_" + flow), name,
-                 rec)
+    write_record("teacher" + ("_unfused" if unfused else "") + tag + ("_huber" if huber else "")
+                 + ("" if flow == "view" else "_" + flow), name, rec)
     return learner
+
+
+@pytest.mark.parametrize("name", ["tiny_qmix", "tiny_vdn", "tiny_iql", "cfg2_qmix"])
+def test_huber_teacher_forced(cases, name, monkeypatch):
+    """The opt-in masked Huber TD loss (mq_config.huber_delta; north_star names it, the reference has L2 only, so
+    parity is against the oracle's Huber branch, unpinned by any reference golden): stats, gradients and the
+    RMSprop step from the oracle's state, with deltas that put transitions in both the quadratic and linear
+    regimes."""
+    case = get_case(cases, name)
+    run_teacher_forced(case, 3, False, monkeypatch, huber=1.0)
 
 
 def test_data_parallel_norm_path_single_rank(cases):

@@ -77,3 +77,37 @@ def test_max_t_filled_ragged(golden_cases):
         ids = c.z["ids"][k]
         b, _ = c.batch(k)
         assert b["filled"].shape[1] == max_t_filled(c.data["filled"][ids])
+
+
+@pytest.mark.parametrize("name", ["tiny_qmix", "tiny_vdn", "tiny_iql"])
+def test_huber_head_matches_torch(golden_cases, name, monkeypatch):
+    """The oracle's opt-in Huber head (no reference counterpart; the L2 head above is pinned to the reference): its
+    loss and d loss / d Q_tot equal torch's huber_loss(td * mask, 0, delta, sum) / mask.sum() and its autograd."""
+    import torch as th
+    import oracle.qlearner_np as onp
+    c = golden_cases[name]
+    delta = 1.0
+    o = OracleQLearner(c.agent_params, c.mixer_params, dict(c.cfg(), huber_delta=delta))
+    b, _ = c.batch(0)
+    fw = o.forward(b, keep_cache=True)
+    seen = {}
+    real_qb = onp.qmix_backward
+    monkeypatch.setattr(onp, "qmix_backward", lambda mp, cache, dy: (seen.setdefault("dy", dy), real_qb(mp, cache, dy))[1])
+    real_ab = onp.agent_backward
+    monkeypatch.setattr(onp, "agent_backward", lambda p, cache, dmac: (seen.setdefault("dmac", dmac), real_ab(p, cache, dmac))[1])
+    o.gradients(b, fw=fw)
+    q = th.tensor(np.asarray(fw["q_tot"], np.float64), requires_grad=True)
+    m = th.tensor(np.asarray(fw["mask"], np.float64))
+    tgt = th.tensor(np.asarray(fw["targets"], np.float64))
+    loss = th.nn.functional.huber_loss((q - tgt) * m, th.zeros_like(q), reduction="sum", delta=delta) / m.sum()
+    loss.backward()
+    ax = np.abs(fw["td"] * fw["mask"])[fw["mask"] > 0]
+    assert (ax <= delta).any() and (ax > delta).any()   # both regimes
+    assert abs(fw["loss"] - loss.item()) <= 1e-5 * abs(loss.item())
+    g = q.grad.numpy()
+    if c.cfg()["mixer"] == "qmix":
+        got = seen["dy"].reshape(g.shape)
+    else:   # vdn / iql: the Q_tot gradient lands on the chosen actions' Q (one per agent)
+        d = seen["dmac"][:, :-1]
+        got = d.sum(-1) if c.cfg()["mixer"] == "none" else d.sum(-1)[..., :1]
+    assert rel_err(got, g) < 1e-5
