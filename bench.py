@@ -119,6 +119,7 @@ def build_workload(cfg_name, device, n_episodes=5000, unique=512, seed=0):
         for k, v in data.items():
             buf.data.transition_data[k][start:start + m] = th.as_tensor(v[:m], device=device)
     buf.episode_lengths[:] = buf.data.transition_data["filled"].sum(1).reshape(-1).cpu().numpy()
+    buf.refresh_avail_bits()   # direct storage writes: rebuild the buffer's avail bitmask (what inserts maintain)
     buf.episodes_in_buffer = n_episodes
     th.manual_seed(seed)   # identical random-init weights on every rank (data-parallel replicas start equal)
     mac = mac_REGISTRY["basic_mac"](buf.scheme, groups, args)
@@ -161,6 +162,7 @@ def build_coma_workload(cfg_name, device, n_episodes=1000, unique=128, seed=0, d
         for k, v in data.items():
             buf.data.transition_data[k][start:start + m] = th.as_tensor(v[:m], device=device)
     buf.episode_lengths[:] = buf.data.transition_data["filled"].sum(1).reshape(-1).cpu().numpy()
+    buf.refresh_avail_bits()   # direct storage writes: rebuild the buffer's avail bitmask (what inserts maintain)
     buf.episodes_in_buffer = n_episodes
     th.manual_seed(seed)   # identical random-init weights on every rank (data-parallel replicas start equal)
     mac = mac_REGISTRY["basic_mac"](buf.scheme, groups, args)

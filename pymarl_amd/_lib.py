@@ -62,7 +62,7 @@ class MQReplay(ctypes.Structure):
         ("avail_actions", ctypes.c_void_p), ("reward", ctypes.c_void_p), ("terminated", ctypes.c_void_p),
         ("filled", ctypes.c_void_p), ("ep_ids", ctypes.c_void_p), ("n_episodes", ctypes.c_int64),
         ("batch_size", ctypes.c_int32), ("t_len", ctypes.c_int32), ("t_stride", ctypes.c_int32),
-        ("ep_ids_host", ctypes.c_void_p),
+        ("ep_ids_host", ctypes.c_void_p), ("avail_bits", ctypes.c_void_p),
     ]
 
 

@@ -343,6 +343,31 @@ class ReplayBuffer(EpisodeBatch):
         self.buffer_index = 0
         self.episodes_in_buffer = 0
         self.episode_lengths = np.zeros(buffer_size, dtype=np.int64)   # sum(filled) per episode, host side
+        # A bitmask view of avail_actions ([N][T][agents] int64, bit a = action a available), kept in step with the
+        # storage by every write path below; the learner's mixer reads 8 bytes per agent row from it instead of
+        # 4 n_actions (mq_replay.avail_bits). Code that writes the storage tensors directly calls refresh_avail_bits.
+        av = self.data.transition_data.get("avail_actions")
+        self.avail_bits = None
+        if av is not None and av.dim() >= 3 and 0 < av.shape[-1] <= 64:
+            self.avail_bits = th.zeros(av.shape[:-1], dtype=th.int64, device=av.device)
+
+    def refresh_avail_bits(self, bs=slice(None)):
+        if self.avail_bits is None:
+            return
+        av = self.data.transition_data["avail_actions"][bs]
+        w = th.ones(av.shape[-1], dtype=th.int64, device=av.device) << th.arange(av.shape[-1], device=av.device)
+        self.avail_bits[bs] = ((av != 0).to(th.int64) * w).sum(-1)   # distinct bits: the sum is the OR
+
+    def update(self, data, bs=slice(None), ts=slice(None), mark_filled=True):
+        super().update(data, bs, ts, mark_filled)
+        if "avail_actions" in data:
+            self.refresh_avail_bits(self._parse_slices((bs, ts))[0])
+
+    def to(self, device):
+        super().to(device)
+        if self.avail_bits is not None:
+            self.avail_bits = self.avail_bits.to(device)
+        return self
 
     def insert_episode_batch(self, ep_batch):
         if self.buffer_index + ep_batch.batch_size <= self.buffer_size:
@@ -369,6 +394,7 @@ class ReplayBuffer(EpisodeBatch):
             elif k in self.data.episode_data:
                 self.data.episode_data[k][:n] = th.as_tensor(v, device=self.device)
         self.episode_lengths[:n] = self.data.transition_data["filled"][:n].sum(1).reshape(-1).cpu().numpy()
+        self.refresh_avail_bits(slice(0, n))
         self.episodes_in_buffer = max(self.episodes_in_buffer, n)
         self.buffer_index = n % self.buffer_size
 

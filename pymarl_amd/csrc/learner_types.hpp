@@ -43,6 +43,7 @@ struct Rep {
   const uint8_t* term;
   const int64_t* filled;
   const int64_t* ep_ids;
+  const uint64_t* avail_bits = nullptr;   // optional bitmask view of avail (mq_replay.avail_bits); NULL: avail
   int32_t nids;                    // > 0: the ids live in `ids` (kernel arguments), ep_ids unused
   int32_t ids[MQ_INLINE_IDS];
   MQ_DEV int64_t ep(int b) const { return nids ? (int64_t)ids[b] : (ep_ids ? ep_ids[b] : (int64_t)b); }

@@ -77,6 +77,15 @@ __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* _
   const float* Qon = w.Q;
   const float* Qtg = w.Q + d.RT() * A;
   float chosen = 0.0f, tmax = 0.0f;
+  // the transition's mask / reward / terminated words, independent of the selection: in flight with it
+  float mask = 0.0f, rew = 0.0f, term = 0.0f;
+  if (valid) {
+    const int64_t slot = ep * d.t_stride + t;
+    mask = (float)rp.filled[slot];
+    if (t > 0) mask *= 1.0f - (float)rp.term[slot - 1];   // q_learner.py:42-43
+    rew = rp.reward[slot];
+    term = (float)rp.term[slot];
+  }
   if constexpr (STREAM) {
     __shared__ float qm[4 * MIXS_MAX];      // the four items' masked selection rows [item][agent][action]
     __shared__ uint8_t avs[4 * MIXS_MAX];   // their avail bits
@@ -84,8 +93,11 @@ __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* _
     const float* qsel_base = d.double_q ? Qon : Qtg;
     float qv[4][MIXS_NPT];
     int32_t avv[4][MIXS_NPT];
+    // the agent lane's action first (its chosen value is one more round trip), then every staging load of the block
+    // (avail as int32 here: per-element bit extraction from mq_replay.avail_bits measured slower, 74 vs 70 us)
+    const int at = (valid && lane < n) ? (int)rp.actions[(ep * d.t_stride + t) * n + lane] : 0;
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {   // every load of the block first
+    for (int it = 0; it < 4; ++it) {
       const int mi = min((int)blockIdx.x * 4 + it, d.M - 1);
       const int ti = (int)fdiv((uint32_t)mi, d.dB), bi = mi - ti * d.B;
       const float* qrow = qsel_base + ((int64_t)(ti + 1) * R + (int64_t)bi * n) * A;
@@ -97,6 +109,7 @@ __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* _
         avv[it][k] = arow[e];
       }
     }
+    if (valid && lane < n) chosen = Qon[((int64_t)t * R + b * n + lane) * A + at];
 #pragma unroll
     for (int it = 0; it < 4; ++it)
 #pragma unroll
@@ -110,8 +123,6 @@ __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* _
     __syncthreads();
     if (valid && lane < n) {
       const int r = b * n + lane;
-      const int at = (int)rp.actions[(ep * d.t_stride + t) * n + lane];
-      chosen = Qon[((int64_t)t * R + r) * A + at];
       const float* row = qm + wv * nA + lane * A;
       float best = 0.0f;
       int cur = 0;
@@ -133,6 +144,8 @@ __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* _
     const float* qn = Qon + ((int64_t)(t + 1) * R + r) * A;
     const float* qt = Qtg + ((int64_t)(t + 1) * R + r) * A;
     const int32_t* av = rp.avail + ((slot + 1) * n + lane) * (int64_t)A;
+    const uint64_t abits = rp.avail_bits ? rp.avail_bits[(slot + 1) * n + lane] : 0;
+    auto avail_at = [&](int a) { return rp.avail_bits ? (int32_t)((abits >> a) & 1u) : av[a]; };
     // argmax over available actions, first index on ties (torch max): the row is fetched in blocks of kMB
     // independent loads so a wave waits on ceil(A / kMB) round trips instead of A
     const float* qsel = d.double_q ? qn : qt;
@@ -146,7 +159,7 @@ __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* _
       for (int u = 0; u < kMB; ++u) {
         const int a = min(a0 + u, A - 1);
         qv[u] = qsel[a];
-        avv[u] = av[a];
+        avv[u] = avail_at(a);
       }
 #pragma unroll
       for (int u = 0; u < kMB; ++u) {
@@ -155,7 +168,7 @@ __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* _
         if (a < A && (a == 0 || v > best)) { best = v; cur = a; }
       }
     }
-    if (d.double_q) tmax = av[cur] ? qt[cur] : kNegMask;
+    if (d.double_q) tmax = avail_at(cur) ? qt[cur] : kNegMask;
     else tmax = best;
     if (curmax_out) curmax_out[(int64_t)t * R + r] = cur;
   }
@@ -163,14 +176,6 @@ __global__ __launch_bounds__(256) void mix_kernel(Dims d, Rep rp, const float* _
   tms[wv][lane] = tmax;
   __syncthreads();
 
-  float mask = 0.0f, rew = 0.0f, term = 0.0f;
-  if (valid) {
-    const int64_t slot = ep * d.t_stride + t;
-    mask = (float)rp.filled[slot];
-    if (t > 0) mask *= 1.0f - (float)rp.term[slot - 1];   // q_learner.py:42-43
-    rew = rp.reward[slot];
-    term = (float)rp.term[slot];
-  }
   const float gamma = d.gamma;
   if (d.mixer == MQ_MIXER_QMIX) {
     const float* hon = w.HYP + (int64_t)m * NH;
@@ -322,12 +327,13 @@ MQ_DEV void mix_fast_row(const Dims& d, const Rep& rp, const float* __restrict__
     const float* qt = Qtg + ((int64_t)(t + 1) * R + r) * A;
     const float* qs_row = d.double_q ? qn : qt;
     const int32_t* av = rp.avail + ((slot + 1) * n + lane) * (int64_t)A;
+    const uint64_t abits = rp.avail_bits ? rp.avail_bits[(slot + 1) * n + lane] : 0;
 #pragma unroll
     for (int u = 0; u < MA; ++u) {
       const int a = min(u, A - 1);
       qsel[u] = qs_row[a];
       qtr[u] = qt[a];
-      avr[u] = av[a];
+      avr[u] = rp.avail_bits ? (int32_t)((abits >> a) & 1u) : av[a];
     }
   }
   const bool e_lane = qmix && valid && lane < E;

@@ -178,7 +178,7 @@ Dims make_dims(const mq_handle* h, const mq_replay* b) {
 Rep make_rep(const mq_replay* b) {
   Rep r;
   r.obs = b->obs; r.state = b->state; r.actions = b->actions; r.avail = b->avail_actions; r.reward = b->reward;
-  r.term = b->terminated; r.filled = b->filled; r.ep_ids = b->ep_ids;
+  r.term = b->terminated; r.filled = b->filled; r.ep_ids = b->ep_ids; r.avail_bits = b->avail_bits;
   r.nids = 0;
   if (b->ep_ids_host && b->batch_size <= MQ_INLINE_IDS) {   // ids in the kernel arguments (check_batch validated)
     r.nids = b->batch_size;

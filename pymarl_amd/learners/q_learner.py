@@ -20,9 +20,9 @@ from __future__ import annotations
 
 import copy
 import ctypes
+import os
 
 import numpy as np
-import os
 
 import torch as th
 from torch.optim import RMSprop
@@ -109,6 +109,10 @@ def replay_view(batch):
             if t.dtype != dt or not t.is_contiguous():
                 raise _lib.MQError("replay field {} must be a contiguous {} tensor".format(k, dt))
             tensors[k] = t
+        bits = getattr(batch.source, "avail_bits", None)
+        if bits is not None and os.environ.get("MQ_AVAIL_BITS", "1") != "0":   # =0: A/B switch, read avail_actions
+            keep.append(bits)
+            rep.avail_bits = bits.data_ptr()
     else:
         src = batch.data.transition_data
         tensors, strides = {}, set()

@@ -575,6 +575,36 @@ def test_mix_stream_bitwise(cases, name, monkeypatch):
     assert outs[0][2] == outs[1][2]
 
 
+@pytest.mark.parametrize("name,generic", [("cfg3_vdn_b128", False), ("cfg3_vdn_b128", True), ("cfg2_qmix", False),
+                                          ("tiny_qmix_full", False), ("cfg3_qmix", True)])
+def test_avail_bits_bitwise(cases, name, generic, monkeypatch):
+    """The mixer's double-Q selection reading the replay buffer's avail bitmask (mq_replay.avail_bits, the default
+    for buffer views) equals it reading avail_actions (MQ_AVAIL_BITS=0) bitwise, in the staged (stream), per-lane
+    (MQ_MIX_GENERIC=1) and fast mixers; the chosen argmax actions too."""
+    from tests.gpu_helpers import build, flat_grads, flat_params
+    case = get_case(cases, name)
+    if generic:
+        monkeypatch.setenv("MQ_MIX_GENERIC", "1")
+    outs = []
+    for bits in ("1", "0"):
+        monkeypatch.setenv("MQ_AVAIL_BITS", bits)
+        args, buf, mac, learner, logger = build(case)
+        assert buf.avail_bits is not None
+        np.random.seed(case.sampler_seed)
+        acts = []
+        for k in range(min(2, len(case.episodes))):
+            batch = buf.sample(case.B)
+            learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
+            acts.append(learner.last_cur_max_actions().cpu().numpy())
+        th.cuda.synchronize()
+        outs.append((flat_params(learner), flat_grads(learner), learner.last_stats(), acts))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]
+    for a, b in zip(outs[0][3], outs[1][3]):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg4_qmix", "cfg1_qmix", "tiny_qmix_full"])
 def test_dwh_in_bptt_grid_bitwise(cases, name, monkeypatch):
     """dW_hyper's tiles appended to the fused BPTT's grid (MQ_DWH_IN_BWD=1; the default for shards past the CU count,

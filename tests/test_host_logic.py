@@ -63,6 +63,32 @@ def test_replay_buffer_wraparound_and_lengths():
     assert list(rb.episode_lengths) == [2, 2, 2, 2, 2]
 
 
+def _packed(av):
+    out = np.zeros(av.shape[:-1], np.uint64)
+    for a in range(av.shape[-1]):
+        out |= (av[..., a] != 0).astype(np.uint64) << np.uint64(a)
+    return out.view(np.int64)
+
+
+@pytest.mark.parametrize("A", [5, 64])
+def test_replay_buffer_avail_bits_follow_every_write(A):
+    """ReplayBuffer.avail_bits (the mixer's bitmask view of avail_actions, mq_replay.avail_bits) equals the packed
+    storage after insert_episode_batch (wraparound included), update() and load_arrays(); bit 63 at A = 64."""
+    rng = np.random.default_rng(0)
+    rb = ReplayBuffer(scheme(A=A), {"agents": 2}, 5, 3)
+    eb = EpisodeBatch(scheme(A=A), {"agents": 2}, 4, 3)
+    for t in range(3):
+        eb.update({"avail_actions": th.from_numpy(rng.integers(0, 3, (4, 2, A)).astype(np.int32))}, ts=t)
+    rb.insert_episode_batch(eb)
+    rb.insert_episode_batch(eb)   # wraps
+    assert np.array_equal(rb.avail_bits.numpy(), _packed(rb["avail_actions"].numpy()))
+    rb.update({"avail_actions": th.ones(2, A, dtype=th.int32)}, bs=1, ts=2)
+    assert np.array_equal(rb.avail_bits.numpy(), _packed(rb["avail_actions"].numpy()))
+    arr = rng.integers(0, 2, (5, 3, 2, A)).astype(np.int32)
+    rb.load_arrays({"avail_actions": arr, "filled": np.ones((5, 3, 1), np.int64)})
+    assert np.array_equal(rb.avail_bits.numpy(), _packed(arr))
+
+
 def test_sample_matches_reference_rng_and_gather():
     rb = ReplayBuffer(scheme(), {"agents": 2}, 10, 4)
     rb.load_arrays({"obs": np.arange(10 * 4 * 2 * 3, dtype=np.float32).reshape(10, 4, 2, 3),
