@@ -56,11 +56,13 @@ CONFIGS = {
 }
 
 
-def algorithmic_flops(phase, n, A, O, S, T, B, E=32, H=64, mixer="qmix", fused_fwd=False, fused_bwd=False):
+def algorithmic_flops(phase, n, A, O, S, T, B, E=32, H=64, mixer="qmix", fused_fwd=False, fused_bwd=False,
+                      hyp_in_fwd=False):
     """fp32 flops one launch of `phase` must do (matmul terms, 2 flop per MAC; elementwise ignored).
 
     fused_fwd / fused_bwd: the one-row-per-workgroup kernels also carry fc1 / W_ih / fc2 (forward) and
-    dW_hh / dW_ih / dX1 / dW1 (backward) — DESIGN.md "Roofline".
+    dW_hh / dW_ih / dX1 / dW1 (backward) — DESIGN.md "Roofline". hyp_in_fwd: the forward launch also runs the QMIX
+    hypernet (the row-pair kernel's waves 4 / 5, or workgroups appended to the one-row-net grid).
     """
     Tp = T + 1
     R = B * n
@@ -83,6 +85,8 @@ def algorithmic_flops(phase, n, A, O, S, T, B, E=32, H=64, mixer="qmix", fused_f
         f["gru_fwd"] = f["fc1"] + f["gi"] + f["gru_fwd"] + f["fc2"]
     if fused_bwd:
         f["gru_bwd"] = f["gru_bwd"] + f["dx1"] + f["dw1"]
+    if hyp_in_fwd:
+        f["gru_fwd"] = f["gru_fwd"] + f["hyper"]
     return f.get(phase)
 
 
@@ -544,6 +548,8 @@ def main():
     plan = learner.last_plan()   # the kernel variants the timed steps run (row tiles, fused kernels, hypernet, mixer)
     fused_fwd = survey.get("fc1", 0.0) == 0.0     # the fused agent forward carries fc1 / W_ih / fc2
     fused_bwd = survey.get("dx1", 0.0) == 0.0     # the fused BPTT carries dX1 / dW1
+    # no hypernet launch of its own under QMIX: the forward carries it
+    hyp_in_fwd = mixer == "qmix" and survey.get("hyper", 0.0) == 0.0
 
     def timed():
         barrier()
@@ -573,13 +579,14 @@ def main():
     if rank == 0:
         if a.phases:
             print(json.dumps({"phase_ms": survey}), file=sys.stderr)
-        fl = algorithmic_flops(dominant, n, A, O, S, T, B, mixer=mixer, fused_fwd=fused_fwd, fused_bwd=fused_bwd)
+        fl = algorithmic_flops(dominant, n, A, O, S, T, B, mixer=mixer, fused_fwd=fused_fwd, fused_bwd=fused_bwd,
+                               hyp_in_fwd=hyp_in_fwd)
         achieved = (fl / (dom_ms * 1e-3) / 1e12) if (fl and dom_ms > 0) else None
         traffic, traffic_src = pmc_traffic(a.config, dominant)
         roof = {"bound": "mfma", "kernel": dominant, "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": (achieved / FP32_PEAK_TFLOPS) if achieved else None,
                 "traffic": traffic, "traffic_source": traffic_src, "launch_ms": dom_ms, "flops_per_launch": fl,
-                "fused": {"fwd": fused_fwd, "bwd": fused_bwd}, "plan": plan}
+                "fused": {"fwd": fused_fwd, "bwd": fused_bwd, "hyp_in_fwd": hyp_in_fwd}, "plan": plan}
         cpu = rollout = None
         if world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(a.config, data)
