@@ -154,7 +154,8 @@ typedef struct mq_plan {
   int32_t rows;          /* R = batch_size * n_agents */
   int32_t fused_fwd;     /* gru_fwd_fused_kernel (1), gru_fwd_pair_kernel (2) or fc1 / gi / gru_fwd<rw_fwd> / fc2 (0) */
   int32_t rw_fwd;
-  int32_t fused_bwd;     /* gru_bwd_fused_kernel (1) or gru_bwd<rw_bwd> / dx1 / dw1 (0) */
+  int32_t fused_bwd;     /* gru_bwd_fused_kernel (1), gru_bwd_pair_kernel with 1 / 2 rows per workgroup (2 / 3),
+                            or gru_bwd<rw_bwd> / dx1 / dw1 (0) */
   int32_t rw_bwd;
   int32_t inline_ids;    /* episode ids in the kernel arguments (1) or read from mq_replay.ep_ids (0) */
   int32_t hyper;         /* MQ_HYP_* */

@@ -27,6 +27,7 @@
 #include "gru_kernels.hpp"
 #include "gru_fwd_fused.hpp"
 #include "gru_fwd_pair.hpp"
+#include "gru_bwd_pair.hpp"
 #include "gru_bwd_fused.hpp"
 #include "gru_tiles.hpp"
 #include "mix_kernels.hpp"
@@ -117,6 +118,8 @@ struct mq_handle {
   // wave of workgroups; MQ_FWD_PAIR=0 keeps the one-row-net kernel, =1 forces the pair (A/B switches)
   int fwd_pair = getenv("MQ_FWD_PAIR") ? atoi(getenv("MQ_FWD_PAIR")) : -1;
   bool pair_hyp_epi = getenv("MQ_PAIR_HYP_EPI") != nullptr;
+  // MQ_BWD_PAIR=1: the one-chain-wave BPTT (gru_bwd_pair.hpp) where the fused BPTT runs (A/B switch)
+  int bwd_pair = getenv("MQ_BWD_PAIR") ? atoi(getenv("MQ_BWD_PAIR")) : 0;
   // MQ_HYP_SCHED=<hex>: the in-forward hypernet's tile schedule (gru_fwd_pair.hpp hyp_tiles_by; tuning switch)
   int hyp_sched = getenv("MQ_HYP_SCHED") ? (int)strtol(getenv("MQ_HYP_SCHED"), nullptr, 16) : kHypSched;
   // MQ_MIX_GENERIC=1: mix_kernel<false> where mix_kernel<true> (staged selection rows) would run (A/B switch)
@@ -598,12 +601,17 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
 #undef MQ_BWD_TILE
     MQ_HIP(hipGetLastError());
   } else if (fused_bwd) {
-    // one row per workgroup: dW_hh / dW_ih / dX1 / dW1 on the chain's idle matrix cores (gru_bwd_fused.hpp)
-    h->nblk_bwd = d.R;
-    h->nsplit_fc1 = d.R;
+    // one row per workgroup: dW_hh / dW_ih / dX1 / dW1 on the chain's idle matrix cores (gru_bwd_fused.hpp); or the
+    // one-chain-wave BPTT (gru_bwd_pair.hpp), two rows per workgroup when the rows exceed the CUs
+    const bool many = device_cus(h) > 0 && d.R > h->num_cu;
+    const bool bpair = h->bwd_pair == 1 && bwd_pair_ok(d.I, d.O, d.A, d.n, RT);
+    const int nr = 1;
+    h->nblk_bwd = (d.R + nr - 1) / nr;
+    h->nsplit_fc1 = h->nblk_bwd;
+    plan.fused_bwd = bpair ? 1 + nr : 1;
     const size_t dyn = ((size_t)2 * d.A * mq::H + d.A) * sizeof(float);
     dwh_in_bwd = c.mixer == MQ_MIXER_QMIX &&
-                 (h->dwh_in_bwd == 1 || (h->dwh_in_bwd < 0 && device_cus(h) > 0 && d.R > h->num_cu));
+                 (h->dwh_in_bwd == 1 || (h->dwh_in_bwd < 0 && many));
     if (dwh_in_bwd) {   // the reduction's dW_hyper blocks, same geometry (see dwh_fused below)
       w.dwh_tj = (d.NH + DWH_T - 1) / DWH_T;
       const int ts = (d.S + 1 + DWH_T - 1) / DWH_T;
@@ -611,10 +619,14 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
       w.dwh_n = w.dwh_tj * ts * w.dwh_ns;
       w.dwh_len = h->len_mix;
       h->nsplit_mix = w.dwh_ns;
-      launch_bwd_fused_dwh(dyn, s, d, rp, (const float*)h->on, L, w, h->len_rnn, (int64_t)mq::H * d.I + mq::H);
+    }
+    const float* P0 = (const float*)h->on;
+    const int64_t l1 = (int64_t)mq::H * d.I + mq::H;
+    if (bpair) {
+      launch_bwd_pair<1>(dwh_in_bwd, s, d, rp, P0, L, w, h->len_rnn, l1);
     } else {
-      launch_bwd_fused(dim3(d.R), dyn, s, d, rp, (const float*)h->on, L, w, h->len_rnn,
-                       (int64_t)mq::H * d.I + mq::H);
+      if (dwh_in_bwd) launch_bwd_fused_dwh(dyn, s, d, rp, P0, L, w, h->len_rnn, l1);
+      else launch_bwd_fused(dim3(d.R), dyn, s, d, rp, P0, L, w, h->len_rnn, l1);
     }
     MQ_HIP(hipGetLastError());
   } else {

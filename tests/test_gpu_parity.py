@@ -362,6 +362,16 @@ def test_forward_pair_switch_teacher_forced(cases, name, steps, pair, monkeypatc
     assert learner.last_plan()["fused_fwd"] == (2 if pair == "1" else 1)
 
 
+@pytest.mark.parametrize("name,steps", [("cfg2_qmix", 3), ("cfg2_qmix_ragged", 3), ("tiny_vdn", 3), ("tiny_iql", 3),
+                                        ("tiny_qmix_bare", 3), ("cfg1_qmix", 3), ("cfg2_vdn", 2), ("cfg1_vdn", 3)])
+def test_bwd_pair_teacher_forced(cases, name, steps, monkeypatch):
+    """The one-chain-wave BPTT (gru_bwd_pair.hpp, MQ_BWD_PAIR=1: a row's chain on one wave, lane = unit, the weight
+    gradients on the other SIMDs) teacher-forced against the oracle: stats, gradients and the RMSprop step."""
+    monkeypatch.setenv("MQ_BWD_PAIR", "1")
+    learner = run_teacher_forced(get_case(cases, name), steps, False, monkeypatch)
+    assert learner.last_plan()["fused_bwd"] == 2
+
+
 @pytest.mark.parametrize("name,steps,flow", [
     ("tiny_qmix", 4, "cpu_to"), ("cfg2_qmix", 3, "cpu_to"), ("cfg2_qmix_ragged", 3, "cpu_to"), ("cfg1_qmix", 4, "cpu_to"),
     ("tiny_vdn", 3, "cpu_to"), ("tiny_qmix", 4, "dense_slice"), ("cfg1_qmix", 4, "dense_slice")])
