@@ -28,6 +28,7 @@
 // [fc1.w | fc1.b]), the workgroup's rows summed; the reduction takes ceil(R / NR) slabs.
 // DWH = 1: workgroups past the rows compute dW_hyper tiles (dwh_body), as gru_bwd_fused_kernel<1>.
 #pragma once
+#include <type_traits>
 #include "gru_bwd_fused.hpp"
 
 namespace mq {
@@ -189,8 +190,20 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   } else {
     // ================================================================== producer waves pw = 0 .. NP-1
     // tiles round-robin over the producers: dW_hh / dW_ih M-tiles (12), dX1 N-tiles and dW1 M-tiles (4)
-    constexpr int MT = (12 + NP - 1) / NP, XT = (4 + NP - 1) / NP;
-    const int pw = wv - NR;
+    // NP = 3 (NR = 1): producer 0 owns dX1 / dW1 tiles 0 and 3 (152 MFMAs a chunk) and so only dW M-tiles 0, 1;
+    // producers 1 and 2 own one dX1 / dW1 tile and five dW M-tiles each (216 / 236 / 236 MFMAs a chunk, against
+    // 280 / 204 / 204 round-robin); producer 0 also takes the fc2 gradients
+    static_assert(NR == 1 && NP == 3, "the producers' tile split and chunk-ahead prefetch assume one row per workgroup");
+    // each producer's code is specialised on its index (tile ownership known at compile time: no branch around each
+    // MFMA group, which also kept hipcc from scheduling LDS operand reads across groups, ISA round 5)
+    auto producer = [&](auto pw_c) {
+    constexpr int PW = decltype(pw_c)::value;
+    constexpr int MT = 5, XT = PW == 0 ? 2 : 1;
+    const int pw = PW;
+    constexpr int mt0 = PW == 0 ? 0 : 2 + 5 * (PW - 1), mtn = PW == 0 ? 2 : 5;
+    auto mtile = [&](int i) { return mt0 + i; };   // this wave's i-th dW M-tile
+    auto mvalid = [&](int i) { return i < mtn; };
+    constexpr int pfc2 = 0;   // the fc2 gradients go to the producer with the fewest MFMAs
     const int g = lane >> 4, c16 = lane & 15;
     const int Kq = (I + 15) / 16 * 4;
     const int nt1 = min(7, Kq / 4);   // dW1 N-tiles
@@ -213,7 +226,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     drain_vmem();
     lds_barrier();   // prologue (the matching barrier of the chains)
     if (cl >= 1) stage_inputs(cl - 1, 0, pw * 64 + lane, 64 * NP);
-    static_assert(NR == 1, "the producers' chunk-ahead fragment prefetch assumes one row per workgroup");
     const int rr = (int)blockIdx.x;
     // HBM fragments of a chunk, prefetched one chunk ahead (in flight across the barrier): X1 (dW_ih's B), the relu
     // mask of this wave's dX1 tiles, XIN (dW1's B), and (producer 0) h_t of the chunk's steps for the fc2 grads
@@ -240,7 +252,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
           const int t = min(t0 + 4 * g + e, Tp - 1);
           x1m[x][e] = w.X1[((int64_t)t * R + rr) * H + 16 * min(pw + NP * x, 3) + c16];
         }
-      if (pw == 0) {
+      if constexpr (PW == pfc2) {
 #pragma unroll
         for (int i = 0; i < FCH; ++i) hst[i] = w.Hs[((int64_t)min(t0 + i, Tp - 1) * R + rr) * H + lane];
       }
@@ -261,8 +273,8 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         for (int jj = 0; jj < 4; ++jj) bv[jj] = ghr[3 * H + 16 * jj + c16];
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
-          const int mt = pw + NP * i;
-          if (mt < 12) {
+          const int mt = mtile(i);
+          if (mvalid(i)) {
             const float av = ghr[16 * mt + c16];
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) acc_hh[i][jj] = mfma16x4(av, bv[jj], acc_hh[i][jj]);
@@ -275,8 +287,8 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         const float* gir = S.gi[z][cb][4 * kb + g];
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
-          const int mt = pw + NP * i;
-          if (mt < 12) {
+          const int mt = mtile(i);
+          if (mvalid(i)) {
             const float av = gir[16 * mt + c16];
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) acc_ih[i][jj] = mfma16x4(av, x1b[kb][jj], acc_ih[i][jj]);
@@ -315,12 +327,12 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
           const float av = S.dxp[pw][4 * kb + g][c16];
 #pragma unroll
           for (int j = 0; j < 7; ++j)
-            if (j < nt1) acc_w1[x][j] = mfma16x4(av, xib[kb][j], acc_w1[x][j]);
+            acc_w1[x][j] = mfma16x4(av, xib[kb][j], acc_w1[x][j]);   // zero B past I
         }
       }
-      // fc2 gradients of the chunk's steps (producer 0): dW2[a_t][k] += dchosen_t h_t[k], t descending; dchosen
+      // fc2 gradients of the chunk's steps (producer pfc2): dW2[a_t][k] += dchosen_t h_t[k], t descending; dchosen
       // and a_t from the chain's records, h_t prefetched
-      if (pw == 0) {
+      if constexpr (PW == pfc2) {
         const int hi = min(t0 + FCH, T) - 1;
 #pragma unroll
         for (int i = FCH - 1; i >= 0; --i) {
@@ -336,8 +348,8 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     // slabs in the MFMA C layout: element (16 tile + 4 g + e, 16 tile' + c16)
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-      const int mt = pw + NP * i;
-      if (mt >= 12) break;
+      const int mt = mtile(i);
+      if (!mvalid(i)) break;
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
@@ -361,6 +373,11 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         }
       S.db1[g][16 * nt + c16] = db1p[x];
     }
+    };
+    const int pwr = wv - NR;
+    if (pwr == 0) producer(std::integral_constant<int, 0>{});
+    else if (pwr == 1) producer(std::integral_constant<int, 1>{});
+    else producer(std::integral_constant<int, 2>{});
     lds_barrier();   // final
   }
   // after the final barrier: dW2 / db2, the chains' bias gradients (rows summed), the fc1 bias
