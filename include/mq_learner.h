@@ -32,7 +32,8 @@ extern "C" {
 enum { MQ_MIXER_NONE = 0, MQ_MIXER_VDN = 1, MQ_MIXER_QMIX = 2 };
 enum { MQ_OK = 0, MQ_ERR_ARG = 1, MQ_ERR_HIP = 2, MQ_ERR_STATE = 3 };
 enum { MQ_NSUMS = 8 };   /* tail of the gradient buffer: sum (td*m)^2 (Huber: sum huber(td*m)), sum m, sum |td*m|, sum Q_tot*m, sum y*m */
-enum { MQ_NSTATS = 8 };  /* loss, grad_norm, td_error_abs, q_taken_mean, target_mean, mask_sum */
+enum { MQ_NSTATS = 8 };  /* loss, grad_norm, td_error_abs, q_taken_mean, target_mean, mask_sum, clip coefficient,
+                           0 (reserved) */
 
 /* Parameter tensors, in the reference's parameters()/state_dict order: RNNAgent (rnn_agent.py:19-21) then
  * QMixer (qmix.py:14-23). mq_param_offsets fills offsets[MQ_P_COUNT + 1] (last = total). */
@@ -154,8 +155,7 @@ typedef struct mq_plan {
   int32_t rows;          /* R = batch_size * n_agents */
   int32_t fused_fwd;     /* gru_fwd_fused_kernel (1), gru_fwd_pair_kernel (2) or fc1 / gi / gru_fwd<rw_fwd> / fc2 (0) */
   int32_t rw_fwd;
-  int32_t fused_bwd;     /* gru_bwd_fused_kernel (1), gru_bwd_pair_kernel with 1 / 2 rows per workgroup (2 / 3),
-                            or gru_bwd<rw_bwd> / dx1 / dw1 (0) */
+  int32_t fused_bwd;     /* gru_bwd_fused_kernel (1) or gru_bwd<rw_bwd> / dx1 / dw1 (0) */
   int32_t rw_bwd;
   int32_t inline_ids;    /* episode ids in the kernel arguments (1) or read from mq_replay.ep_ids (0) */
   int32_t hyper;         /* MQ_HYP_* */

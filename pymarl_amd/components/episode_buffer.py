@@ -343,13 +343,26 @@ class ReplayBuffer(EpisodeBatch):
         self.buffer_index = 0
         self.episodes_in_buffer = 0
         self.episode_lengths = np.zeros(buffer_size, dtype=np.int64)   # sum(filled) per episode, host side
-        # A bitmask view of avail_actions ([N][T][agents] int64, bit a = action a available), kept in step with the
-        # storage by every write path below; the learner's mixer reads 8 bytes per agent row from it instead of
-        # 4 n_actions (mq_replay.avail_bits). Code that writes the storage tensors directly calls refresh_avail_bits.
+        # A bitmask view of avail_actions ([N][T][agents] int64, bit a = action a available); the learner's mixer
+        # reads 8 bytes per agent row from it instead of 4 n_actions (mq_replay.avail_bits). It is a derived cache, so
+        # it remembers which storage it was built from: (the avail_actions tensor's data pointer, its in-place write
+        # counter `_version`, which every write bumps, through views and indexing included). avail_bits_current()
+        # rebuilds it whenever that stamp moved, so a write that bypasses update() (e.g.
+        # `transition_data["avail_actions"][...] = x`, or a replaced tensor) can never leave the mixer reading stale
+        # bits; the write paths below keep it current cheaply, rebuilding only the rows they wrote.
         av = self.data.transition_data.get("avail_actions")
         self.avail_bits = None
+        self._bits_at = None
         if av is not None and av.dim() >= 3 and 0 < av.shape[-1] <= 64:
             self.avail_bits = th.zeros(av.shape[:-1], dtype=th.int64, device=av.device)
+            self._bits_at = self._avail_stamp()   # zero storage, zero bits
+
+    def _avail_stamp(self):
+        av = self.data.transition_data.get("avail_actions")
+        return None if av is None else (av.data_ptr(), av._version)
+
+    def _bits_fresh(self):
+        return self.avail_bits is not None and self._bits_at == self._avail_stamp()
 
     def refresh_avail_bits(self, bs=slice(None)):
         if self.avail_bits is None:
@@ -357,16 +370,31 @@ class ReplayBuffer(EpisodeBatch):
         av = self.data.transition_data["avail_actions"][bs]
         w = th.ones(av.shape[-1], dtype=th.int64, device=av.device) << th.arange(av.shape[-1], device=av.device)
         self.avail_bits[bs] = ((av != 0).to(th.int64) * w).sum(-1)   # distinct bits: the sum is the OR
+        self._bits_at = self._avail_stamp()
+
+    def avail_bits_current(self):
+        """The avail bitmask, rebuilt first if avail_actions was written since it was last built (None when the
+        buffer has no bitmask: no avail_actions, or more than 64 actions)."""
+        if self.avail_bits is None:
+            return None
+        if not self._bits_fresh():
+            self.refresh_avail_bits()
+        return self.avail_bits
 
     def update(self, data, bs=slice(None), ts=slice(None), mark_filled=True):
+        fresh = self._bits_fresh()   # before this write: were the bits current?
         super().update(data, bs, ts, mark_filled)
         if "avail_actions" in data:
-            self.refresh_avail_bits(self._parse_slices((bs, ts))[0])
+            # only the written rows, unless something else wrote the storage since the last rebuild
+            self.refresh_avail_bits(self._parse_slices((bs, ts))[0] if fresh else slice(None))
 
     def to(self, device):
+        fresh = self._bits_fresh()
         super().to(device)
         if self.avail_bits is not None:
             self.avail_bits = self.avail_bits.to(device)
+            if fresh:
+                self._bits_at = self._avail_stamp()
         return self
 
     def insert_episode_batch(self, ep_batch):
@@ -388,13 +416,14 @@ class ReplayBuffer(EpisodeBatch):
     def load_arrays(self, arrays, n_episodes=None):
         """Bulk-fill the storage from numpy/torch arrays in the scheme layout (synthetic replay, checkpoints)."""
         n = n_episodes if n_episodes is not None else len(next(iter(arrays.values())))
+        fresh = self._bits_fresh()
         for k, v in arrays.items():
             if k in self.data.transition_data:
                 self.data.transition_data[k][:n] = th.as_tensor(v, device=self.device)
             elif k in self.data.episode_data:
                 self.data.episode_data[k][:n] = th.as_tensor(v, device=self.device)
         self.episode_lengths[:n] = self.data.transition_data["filled"][:n].sum(1).reshape(-1).cpu().numpy()
-        self.refresh_avail_bits(slice(0, n))
+        self.refresh_avail_bits(slice(0, n) if fresh else slice(None))
         self.episodes_in_buffer = max(self.episodes_in_buffer, n)
         self.buffer_index = n % self.buffer_size
 

@@ -28,7 +28,7 @@
 // accumulators) are summed in other fixed orders, so the two paths agree to float rounding, not bitwise. The RMSprop
 // update is applied at the end of its own step instead of inside the next step's staging. Both paths are checked
 // against the oracle and against each other (tests/test_gpu_coma.py).
-// Measured at cfg5 (MMM2 shape, R = 80, Kc = 868, G = 64; MQ_COMA_CHAIN_TRACE=1 prints workgroup 0's phase spans):
+// Measured at cfg5 (MMM2 shape, R = 80, Kc = 868, G = 64; MQ_DIAG coma_trace prints workgroup 0's phase spans):
 // DESIGN.md §3b.
 #pragma once
 #include "coma_kernels.hpp"
@@ -101,8 +101,8 @@ struct CChain {
   unsigned* flagB;    // [NHEAD] phase-B-done step tags of the heads
   int NK, NG, NHEAD;
   OptHP hp;
-  unsigned long long* trace;   // optional (MQ_COMA_CHAIN_TRACE): workgroup 0's phase timestamps, [16 steps][8]
-  int fault_wg;                // test hook (MQ_COMA_CHAIN_FAULT): this workgroup never flags its phase A of the
+  unsigned long long* trace;   // optional (MQ_DIAG coma_trace): workgroup 0's phase timestamps, [16 steps][8]
+  int fault_wg;                // test hook (MQ_DIAG coma_fault): this workgroup never flags its phase A of the
                                // second live step, so the heads time out (-1: none)
 };
 

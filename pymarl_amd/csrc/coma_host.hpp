@@ -24,12 +24,12 @@ struct mc_handle {
   float *dL, *dHo, *pi, *ppart, *slab_fc2, *red_tmp, *norm_part;
   int last_T = 0, last_R = 0, last_Rc = 0;
   bool timing = false;
-  // persistent critic chain (coma_chain.hpp): off with MQ_COMA_CHAIN=0, or where cc_ok rejects the shape
+  // persistent critic chain (coma_chain.hpp): off with MQ_PLAN coma_chain=0, or where cc_ok rejects the shape
   bool chain_env = true;
   int num_cu = 0;
   bool chain_attr = false;
   int last_path = -1;
-  unsigned long long* chain_trace = nullptr;   // MQ_COMA_CHAIN_TRACE=1: phase timestamps printed after each train
+  unsigned long long* chain_trace = nullptr;   // MQ_DIAG coma_trace: phase timestamps printed after each train
   // data parallel (mc_set_data_parallel)
   mc_allreduce_fn dp_fn = nullptr;
   void* dp_ctx = nullptr;
@@ -222,8 +222,7 @@ int mc_create(const mc_config* cfg, mc_handle** out) {
   h->dL = b + offs[k++]; h->dHo = b + offs[k++]; h->pi = b + offs[k++]; h->ppart = b + offs[k++];
   h->slab_fc2 = b + offs[k++]; h->red_tmp = b + offs[k++]; h->norm_part = b + offs[k++];
   h->Pbak = b + offs[k++];
-  const char* ev = std::getenv("MQ_COMA_CHAIN");
-  h->chain_env = !(ev && ev[0] == '0');
+  h->chain_env = plan_int("coma_chain", 1) != 0;   // MQ_PLAN coma_chain=0: three launches per critic step
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&h->num_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -380,8 +379,9 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
     }
     return MQ_OK;
   };
-  const char* ov = std::getenv("MQ_COMA_OVERLAP");
-  const bool try_overlap = !dp && !h->timing && !(ov && ov[0] == '0') && h->chain_env && cc_ok(R, A, h->Kc, h->num_cu);
+  // MQ_PLAN coma_overlap=0: the actor's agent unroll stays on the caller's stream
+  const bool try_overlap = !dp && !h->timing && plan_int("coma_overlap", 1) != 0 && h->chain_env &&
+                           cc_ok(R, A, h->Kc, h->num_cu);
   if (try_overlap) {
     MQ_HIP(ensure_side(ah));
     MQ_HIP(hipEventRecord(ah->ev_fork, s));   // before the chain: the side stream does not wait for it
@@ -399,16 +399,16 @@ int mc_train_step(mc_handle* h, const mq_replay* batch, float epsilon, void* str
     cc.crec = h->crec; cc.cstate = h->cstate; cc.sync = (unsigned*)(h->cstate + 2);   // zeroed above
     cc.NK = cc_nk(h->Kc); cc.NG = 8 * cc.NK; cc.NHEAD = (R + 15) / 16;
     cc.hp = ca.hp;
-    const char* tr = std::getenv("MQ_COMA_CHAIN_TRACE");
-    if (tr && tr[0] == '1' && !h->chain_trace) MQ_HIP(hipMalloc(&h->chain_trace, 16 * 8 * sizeof(unsigned long long)));
+    if (env_item("MQ_DIAG", "coma_trace") && !h->chain_trace)
+      MQ_HIP(hipMalloc(&h->chain_trace, 16 * 8 * sizeof(unsigned long long)));
     cc.trace = h->chain_trace;
-    const char* fe = std::getenv("MQ_COMA_CHAIN_FAULT");   // test hook: a workgroup that stops flagging
-    cc.fault_wg = fe ? std::atoi(fe) : -1;
+    cc.fault_wg = env_int("MQ_DIAG", "coma_fault", -1);   // test hook: a workgroup that stops flagging
     // cnorm: [0, 2 G) the norm granules, [512, 512 + G) flagA, [768, 768 + NHEAD) flagB; no stale step tags
     cc.flagA = (unsigned*)(h->cnorm + 512);
     cc.flagB = (unsigned*)(h->cnorm + 768);
     MQ_HIP(hipMemsetAsync(h->cnorm, 0, 1024 * sizeof(float), s));
     const size_t lds = cc_lds_bytes(A);
+    MQ_LDS(coma_chain_kernel, lds);
     if (!h->chain_attr) {
       MQ_HIP(hipFuncSetAttribute((const void*)coma_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       h->chain_attr = true;

@@ -41,13 +41,16 @@ static_assert(sizeof(PairLds) - offsetof(PairLds, hs) >= 2 * G3 * PSP * sizeof(f
 
 inline bool pair_fwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_fwd_ok(I, O, A, n, RT); }
 
-// STAMP (diagnostic, MQ_PAIR_STAMP; Tp <= 512): s_memtime stamps of the first 8 workgroups (cdna_hip_programming.md
+// STAMP (diagnostic, MQ_DIAG pair_stamp=<file>; Tp <= 512): s_memtime stamps of the first 8 workgroups (cdna_hip_programming.md
 // §7 form: s_memtime + lgkmcnt(0) in one asm statement), kept in LDS and written to w.slab_rnn as uint32
 // [block][16 + 2 * 512] at the end: [0] kernel entry, [1] recurrence loop start, [2] its end, [3] producers'
 // prologue done, [4] the hypernet epilogue's end, producers' [5] loads issued, [6] loads landed, [7] X1(0..1) done,
-// [8] GI(0) done, [9] recurrence's W_hh landed; [16 + t] the recurrence's step t end; [16 + 512 + t] the producers'
+// [8] GI(0) done, [9] recurrence's W_hh landed, [11 .. 14] the hypernet waves' S3 .. chunk-0 intervals, [15] their
+// exit; producer 0's prologue: [16] after S1, [17] its gather and W1 loads issued, [18] after S2, [19] xin(0) stored,
+// [20] after S3, [21] after S4, [22] after S5; [32 + t] the recurrence's step t end; [32 + 512 + t] the producers'
 // arrival at the barrier closing the chunk of step t (chunk ends only).
-constexpr int PST = 16 + 2 * 512;
+constexpr int PSH = 32;   // header slots
+constexpr int PST = PSH + 2 * 512;
 MQ_DEV uint32_t stamp_now() {
   uint64_t t;
   __builtin_amdgcn_sched_barrier(0);
@@ -293,7 +296,7 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
         S.hs[z][c & 1][p][j] = h1;   // read back by this wave's next step (in-order LDS, no barrier)
         // the online record goes to HBM through the producers (one chunk later), not from this wave
         if (online) S.grec[c & 1][p][j] = f32x4{rg, zg, ng, ghn};
-        if (z == 0) stamp(16 + t);
+        if (z == 0) stamp(PSH + t);
       }
       lds_barrier();   // chunk c's h history complete; chunk c + 1's GI staged
     }
@@ -331,7 +334,9 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
     f_ld = *(const int*)(rp.filled + slot0 + t);
     a_ld = *(const int*)(rp.actions + (slot0 + t) * n + ag);
   };
+  if (pw == 0) stamp(16);
   issue_gather(0);
+  if (pw == 0) stamp(17);
   // register-resident weights of both nets: W1 (fc1 B fragments of N-tile pw), W_ih (3 N-tiles), W2 (K = 64), as
   // 16-byte loads (W_ih / W2 rows are 64 floats at offsets that are multiples of 4; W1's rows when I % 4 == 0,
   // otherwise element by element), every load of the prologue in flight at once
@@ -480,12 +485,15 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
   // xin(1) -> X1(0), X1(1) -> GI(0); xin(2) staged
   if (pw == 0) stamp(5);
   lds_barrier();   // S2: the recurrences have copied W_hh out of the staging area
+  if (pw == 0) stamp(18);
   stage_rows((int)L.o[MQ_P_RNN_W_IH], 384, 128 + ptid);
   drain_vmem();
   if (pw == 0) stamp(6);
   store_gather(0);
   if (cl >= 1) issue_gather(1);
+  if (pw == 0) stamp(19);
   lds_barrier();   // S3: W_ih staged
+  if (pw == 0) stamp(20);
 #pragma unroll
   for (int z = 0; z < 2; ++z)
 #pragma unroll
@@ -502,6 +510,7 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
   if (cl >= 2) issue_gather(2);
   if (pw == 0) stamp(3);
   lds_barrier();   // S4: W_ih copied out (the staging area is free), xin(0), xin(1)
+  if (pw == 0) stamp(21);
 #pragma unroll
   for (int z = 0; z < 2; ++z) {
     fc1(z, 0);
@@ -509,6 +518,7 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
   }
   if (pw == 0) stamp(7);
   lds_barrier();   // S5: X1(0), X1(1); xin(0) free
+  if (pw == 0) stamp(22);
   if (cl >= 2) { store_gather(2); if (cl >= 3) issue_gather(3); }
 #pragma unroll
   for (int z = 0; z < 2; ++z) gi(z, 0);
@@ -524,7 +534,7 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
     if (c + 1 <= cl) { gi(0, c + 1); gi(1, c + 1); }
     if (c + 2 <= cl) { fc1(0, c + 2); fc1(1, c + 2); }
     if (c + 3 <= cl) { store_gather(c + 3); if (c + 4 <= cl) issue_gather(c + 4); }
-    if (pw == 0) stamp(16 + 512 + min(FCH * c + FCH - 1, Tp - 1));
+    if (pw == 0) stamp(PSH + 512 + min(FCH * c + FCH - 1, Tp - 1));
     lds_barrier();
   }
   if (pw < 2) fc2(cl);   // the last chunk's h history is complete after the final barrier

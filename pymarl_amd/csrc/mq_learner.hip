@@ -27,7 +27,6 @@
 #include "gru_kernels.hpp"
 #include "gru_fwd_fused.hpp"
 #include "gru_fwd_pair.hpp"
-#include "gru_bwd_pair.hpp"
 #include "gru_bwd_fused.hpp"
 #include "gru_tiles.hpp"
 #include "mix_kernels.hpp"
@@ -35,6 +34,7 @@
 #include "dwh_kernel.hpp"
 #include "optim_kernels.hpp"
 #include "module_fwd.hpp"
+#include "switches.hpp"
 
 using namespace mq;
 
@@ -48,6 +48,46 @@ int set_err(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+
+// A kernel's static LDS plus a launch's dynamic LDS against the CU's LDS (160 KB on gfx950), checked before the
+// launch (the static size is looked up once per kernel). A dispatch past it aborts the whole queue
+// (HSA_STATUS_ERROR_INVALID_ALLOCATION), which HIP then reports at the next runtime call as "an illegal memory access
+// was encountered", far from its cause: the round-5 fault of a stamped BPTT build was exactly that.
+int lds_fits(const void* fn, size_t dyn, const char* what) {
+  static std::mutex mu;
+  static std::vector<std::pair<const void*, size_t>> known;
+  static int limit = 0;
+  size_t st = 0;
+  bool found = false;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    for (const auto& k : known)
+      if (k.first == fn) { st = k.second; found = true; break; }
+  }
+  if (!found) {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, fn) != hipSuccess) return set_err(MQ_ERR_HIP, std::string(what) + ": hipFuncGetAttributes");
+    st = fa.sharedSizeBytes;
+    std::lock_guard<std::mutex> lk(mu);
+    known.emplace_back(fn, st);
+    if (limit == 0) {
+      int dev = 0, v = 0;
+      limit = (hipGetDevice(&dev) == hipSuccess &&
+               hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) == hipSuccess && v > 0)
+                  ? v : 160 * 1024;
+    }
+  }
+  if (st + dyn > (size_t)limit)
+    return set_err(MQ_ERR_ARG, std::string(what) + " needs " + std::to_string(st) + " B of static + " +
+                                   std::to_string(dyn) + " B of dynamic LDS, past the " + std::to_string(limit) +
+                                   " B a workgroup can have");
+  return MQ_OK;
+}
+#define MQ_LDS(fn, dyn)                                                        \
+  do {                                                                         \
+    const int _rc = lds_fits((const void*)(fn), (size_t)(dyn), #fn);          \
+    if (_rc) return _rc;                                                       \
+  } while (0)
 
 #define MQ_HIP(expr)                                                                        \
   do {                                                                                      \
@@ -88,8 +128,9 @@ struct mq_handle {
   Dims last;
   mq_plan plan{};
   int nsplit_fc1 = 1, nsplit_mix = 1, nblk_bwd = 1, nblk_mix = 1, n_norm_part = 0;
-  bool force_unfused = getenv("MQ_UNFUSED_FWD") != nullptr;       // A/B switch for the fused agent forward
-  bool force_unfused_bwd = getenv("MQ_UNFUSED_BWD") != nullptr;   // A/B switch for the fused BPTT
+  // plan overrides (switches.hpp MQ_PLAN; A/B runs and tests, read once here)
+  bool force_unfused = plan_flag("unfused_fwd");       // the unfused forward (GEMMs around gru_fwd<RW>)
+  bool force_unfused_bwd = plan_flag("unfused_bwd");   // the unfused BPTT (gru_bwd<RW> + dX1 / dW1 GEMMs)
   // rows up to which the fused BPTT (one row per workgroup, one workgroup per CU) is used: past the CU count the
   // rows run as a second wave of workgroups, which still beats gru_bwd<2> + dX1 + dW1 at configs[3]'s shard
   // (R = 320; round 3)
@@ -97,8 +138,8 @@ struct mq_handle {
   // m-slices of the dW_hyper pass (A/B at cfg2, DESIGN §3: 4 / 8 / 16 / 32 -> 238.5 / 235.1 / 236.3 / 237.4 us)
   static constexpr int dwh_split = 8;
   // the row-tile MFMA forward / BPTT (gru_tiles.hpp) for batches past the one-row fused kernels (R > 512 rows);
-  // MQ_ROW_TILES=1 forces it on any batch it can take (tests), =0 turns it off (A/B: the unfused GEMM path)
-  int row_tiles = getenv("MQ_ROW_TILES") ? atoi(getenv("MQ_ROW_TILES")) : -1;
+  // row_tiles=1 forces it on any batch it can take (tests), =0 turns it off (A/B: the unfused GEMM path)
+  int row_tiles = plan_int("row_tiles", -1);
   bool dp = false;   // gradient buffer is summed across ranks between mq_forward_backward and mq_apply
   ncclComm_t comm = nullptr;   // mq_comm_attach / mq_comm_use: the library all-reduces the grad buffer itself
   int comm_world = 0;
@@ -107,23 +148,18 @@ struct mq_handle {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // QMIX hypernet workgroups appended to the fused forward's grid (gru_fwd_fused.hpp hyper_fwd_body) when the
   // forward's 2R row-nets exceed two per CU: its second wave leaves CUs idle, and the hypernet fills them
-  // (configs[3]'s shard, R = 320: 0.364 -> 0.346 ms a step). In one wave (cfg2, R = 256) it measured no faster than
-  // hyper_ws_kernel after the forward, which stays. MQ_HYP_IN_FWD=0 never appends, =1 always (A/B switches; the HYP
-  // is bitwise the same either way)
-  int hyp_in_fwd = getenv("MQ_HYP_IN_FWD") ? atoi(getenv("MQ_HYP_IN_FWD")) : -1;
+  // (configs[3]'s shard, R = 320: 0.364 -> 0.346 ms a step). hyp_in_fwd=0 never appends (and launches hyper_ws_kernel
+  // after the row-pair forward instead of running the hypernet inside it), =1 always (HYP bitwise the same either way)
+  int hyp_in_fwd = plan_int("hyp_in_fwd", -1);
   // dW_hyper's tiles appended to the fused BPTT's grid (gru_bwd_fused.hpp, DWH = 1) when its rows exceed the CUs
-  // (a second wave of rows leaves CUs idle); MQ_DWH_IN_BWD=0 never, =1 always (A/B switches; bitwise either way)
-  int dwh_in_bwd = getenv("MQ_DWH_IN_BWD") ? atoi(getenv("MQ_DWH_IN_BWD")) : -1;
+  // (a second wave of rows leaves CUs idle); dwh_in_bwd=0 never, =1 always (bitwise either way)
+  int dwh_in_bwd = plan_int("dwh_in_bwd", -1);
   // the row-pair forward (gru_fwd_pair.hpp: both nets of a row in one workgroup, one per CU) when the rows fit one
-  // wave of workgroups; MQ_FWD_PAIR=0 keeps the one-row-net kernel, =1 forces the pair (A/B switches)
-  int fwd_pair = getenv("MQ_FWD_PAIR") ? atoi(getenv("MQ_FWD_PAIR")) : -1;
-  bool pair_hyp_epi = getenv("MQ_PAIR_HYP_EPI") != nullptr;
-  // MQ_BWD_PAIR=1: the one-chain-wave BPTT (gru_bwd_pair.hpp) where the fused BPTT runs (A/B switch)
-  int bwd_pair = getenv("MQ_BWD_PAIR") ? atoi(getenv("MQ_BWD_PAIR")) : 0;
-  // MQ_HYP_SCHED=<hex>: the in-forward hypernet's tile schedule (gru_fwd_pair.hpp hyp_tiles_by; tuning switch)
-  int hyp_sched = getenv("MQ_HYP_SCHED") ? (int)strtol(getenv("MQ_HYP_SCHED"), nullptr, 16) : kHypSched;
-  // MQ_MIX_GENERIC=1: mix_kernel<false> where mix_kernel<true> (staged selection rows) would run (A/B switch)
-  bool mix_generic = getenv("MQ_MIX_GENERIC") != nullptr;
+  // wave of workgroups; fwd_pair=0 keeps the one-row-net kernel, =1 forces the pair
+  int fwd_pair = plan_int("fwd_pair", -1);
+  bool pair_hyp_epi = plan_flag("pair_hyp_epi");   // the pair forward's hypernet as its epilogue, not on waves 4 / 5
+  // mix_kernel<false> where mix_kernel<true> (staged selection rows) would run
+  bool mix_generic = plan_flag("mix_generic");
   int num_cu = 0;
   // timing: a ring of `slots` steps x PH_N (start, stop) event pairs; phases outside `mask` are not recorded
   int slots = 0;
@@ -480,8 +516,8 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     // one row per workgroup: fc1 / W_ih / fc2 ride on the recurrence's idle matrix cores (gru_fwd_fused.hpp)
     pt.begin(PH_GRUF);
     const bool two_waves = device_cus(h) > 0 && d.R > h->num_cu;   // 2R row-nets at two per CU
-    // the row-pair forward when the rows fit one wave of workgroups (MQ_FWD_PAIR=1 forces it, =0 keeps the one-row-net
-    // kernel); MQ_HYP_IN_FWD=1 asks for the one-row-net kernel with the hypernet appended to its grid
+    // the row-pair forward when the rows fit one wave of workgroups (MQ_PLAN fwd_pair=1 forces it, =0 keeps the one-row-net
+    // kernel); hyp_in_fwd=1 asks for the one-row-net kernel with the hypernet appended to its grid
     const bool pair = h->hyp_in_fwd != 1 && pair_fwd_ok(d.I, d.O, d.A, d.n, RT) &&
                       (h->fwd_pair == 1 || (h->fwd_pair < 0 && !two_waves && device_cus(h) > 0));
     hyp_in_fwd = !pair && (h->hyp_in_fwd == 1 || (h->hyp_in_fwd < 0 && two_waves)) && c.mixer == MQ_MIXER_QMIX &&
@@ -491,21 +527,24 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
       launch_fwd_fused_hyp(s, d, rp, (const float*)h->on, (const float*)h->tg, L, w);
     } else if (pair) {
       plan.fused_fwd = 2;
-      // the QMIX hypernet as the pair kernel's epilogue (MQ_HYP_IN_FWD=0 keeps hyper_ws_kernel after it)
+      // the QMIX hypernet as the pair kernel's epilogue (hyp_in_fwd=0 keeps hyper_ws_kernel after it)
       hyp_in_fwd = h->hyp_in_fwd != 0 && c.mixer == MQ_MIXER_QMIX && hyper_ws_ok(d.S, d.E, d.NH, d.M) &&
                    hyf_ok(d.S, d.E, d.NH, d.M);
       if (hyp_in_fwd) plan.hyper = MQ_HYP_WS;
-      const char* stamp_path = getenv("MQ_PAIR_STAMP");   // diagnostic: step stamps of the first 8 workgroups
+      std::string stamp_path;   // diagnostic (MQ_DIAG pair_stamp=<file>): step stamps of the first 8 workgroups
+      const bool want_stamp = env_item("MQ_DIAG", "pair_stamp", &stamp_path) && !stamp_path.empty();
+      const int hsched = env_int("MQ_DIAG", "hyp_sched", kHypSched, 16);   // tuning: the in-loop tile schedule
       // on waves 4 / 5 inside the kernel when every hypernet block has a workgroup, else as its epilogue
-      // (MQ_PAIR_HYP_EPI forces the epilogue)
+      // (pair_hyp_epi forces the epilogue)
       const int pair_hyp = !hyp_in_fwd ? 0 : (2 * ((d.M + 31) / 32) <= d.R && !h->pair_hyp_epi) ? 2 : 1;
-      launch_fwd_pair(s, d, rp, (const float*)h->on, (const float*)h->tg, L, w, pair_hyp,
-                      stamp_path != nullptr && d.Tp <= 512, h->hyp_sched);
-      if (stamp_path && FCH * d.O <= 256 * 5 && d.Tp <= 512) {
+      // the stamp build has the 5-slot gather only: shapes past it run unstamped (never a partial gather)
+      const bool stamp = want_stamp && d.Tp <= 512 && FCH * d.O <= 256 * 5;
+      launch_fwd_pair(s, d, rp, (const float*)h->on, (const float*)h->tg, L, w, pair_hyp, stamp, hsched);
+      if (stamp) {
         std::vector<uint32_t> st((size_t)8 * PST);
         MQ_HIP(hipMemcpyAsync(st.data(), w.slab_rnn, st.size() * 4, hipMemcpyDeviceToHost, s));
         MQ_HIP(hipStreamSynchronize(s));
-        if (FILE* f = fopen(stamp_path, "ab")) { fwrite(st.data(), 4, st.size(), f); fclose(f); }
+        if (FILE* f = fopen(stamp_path.c_str(), "ab")) { fwrite(st.data(), 4, st.size(), f); fclose(f); }
       }
     } else {
       launch_fwd_fused(dim3(d.R, 2), s, d, rp, (const float*)h->on, (const float*)h->tg, L, w);
@@ -544,6 +583,7 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     if (hyper_ws_ok(d.S, d.E, d.NH, d.M)) {
       plan.hyper = MQ_HYP_WS;
       // wave-specialised weight streaming (hyper_kernel.hpp)
+      MQ_LDS(hyper_ws_kernel<0>, hyper_ws_lds_bytes(d.S));
       hipLaunchKernelGGL(hyper_ws_kernel<0>, dim3((d.M + HYR - 1) / HYR, 2), dim3(HYWS_THREADS),
                          hyper_ws_lds_bytes(d.S), s, d, rp, (const float*)h->on, (const float*)h->tg, L, w.HYP,
                          w.S0);
@@ -551,6 +591,7 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     } else if (hyper_ok(d.S, d.NH)) {
       plan.hyper = MQ_HYP_LDS;
       const size_t dyn = HyperGeom(d.S, d.NH).lds_bytes();
+      MQ_LDS(hyper_kernel<0>, dyn);
       hipLaunchKernelGGL(hyper_kernel<0>, dim3((d.M + HYR - 1) / HYR, 2), dim3(256), dyn, s, d, rp,
                          (const float*)h->on, (const float*)h->tg, L, w.HYP, w.S0);
       MQ_HIP(hipGetLastError());
@@ -601,14 +642,10 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
 #undef MQ_BWD_TILE
     MQ_HIP(hipGetLastError());
   } else if (fused_bwd) {
-    // one row per workgroup: dW_hh / dW_ih / dX1 / dW1 on the chain's idle matrix cores (gru_bwd_fused.hpp); or the
-    // one-chain-wave BPTT (gru_bwd_pair.hpp), two rows per workgroup when the rows exceed the CUs
-    const bool many = device_cus(h) > 0 && d.R > h->num_cu;
-    const bool bpair = h->bwd_pair == 1 && bwd_pair_ok(d.I, d.O, d.A, d.n, RT);
-    const int nr = 1;
-    h->nblk_bwd = (d.R + nr - 1) / nr;
+    // one row per workgroup: dW_hh / dW_ih / dX1 / dW1 on the chain's idle matrix cores (gru_bwd_fused.hpp)
+    const bool many = device_cus(h) > 0 && d.R > h->num_cu;   // a second wave of rows leaves CUs idle
+    h->nblk_bwd = d.R;
     h->nsplit_fc1 = h->nblk_bwd;
-    plan.fused_bwd = bpair ? 1 + nr : 1;
     const size_t dyn = ((size_t)2 * d.A * mq::H + d.A) * sizeof(float);
     dwh_in_bwd = c.mixer == MQ_MIXER_QMIX &&
                  (h->dwh_in_bwd == 1 || (h->dwh_in_bwd < 0 && many));
@@ -622,16 +659,18 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     }
     const float* P0 = (const float*)h->on;
     const int64_t l1 = (int64_t)mq::H * d.I + mq::H;
-    if (bpair) {
-      launch_bwd_pair<1>(dwh_in_bwd, s, d, rp, P0, L, w, h->len_rnn, l1);
-    } else {
-      if (dwh_in_bwd) launch_bwd_fused_dwh(dyn, s, d, rp, P0, L, w, h->len_rnn, l1);
-      else launch_bwd_fused(dim3(d.R), dyn, s, d, rp, P0, L, w, h->len_rnn, l1);
-    }
+    if (dwh_in_bwd) MQ_LDS(gru_bwd_fused_kernel<1>, dyn);
+    else MQ_LDS(gru_bwd_fused_kernel<0>, dyn);
+    if (dwh_in_bwd) launch_bwd_fused_dwh(dyn, s, d, rp, P0, L, w, h->len_rnn, l1);
+    else launch_bwd_fused(dim3(d.R), dyn, s, d, rp, P0, L, w, h->len_rnn, l1);
     MQ_HIP(hipGetLastError());
   } else {
     {
       // RW >= 4 spills the 96 role registers + per-row prefetch sets at 512 threads; cap at 2
+      const size_t dyn = ((size_t)2 * d.A * mq::H + d.A) * sizeof(float);
+      if (rw_bwd == 1) MQ_LDS(gru_bwd_kernel<1>, dyn);
+      else if (rw_bwd == 2) MQ_LDS(gru_bwd_kernel<2>, dyn);
+      else MQ_LDS(gru_bwd_kernel<4>, dyn);
       hipError_t e = rw_bwd == 1 ? launch_gru_bwd<1>(d, rp, h, L, w, s, &h->nblk_bwd)
                    : rw_bwd == 2 ? launch_gru_bwd<2>(d, rp, h, L, w, s, &h->nblk_bwd)
                                  : launch_gru_bwd<4>(d, rp, h, L, w, s, &h->nblk_bwd);

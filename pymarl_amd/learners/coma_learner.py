@@ -135,7 +135,7 @@ class COMALearner:
     def _get_handle(self, batch):
         T = batch.source.max_seq_length if is_replay_view(batch) else batch.max_seq_length
         need_b = max(batch.batch_size, getattr(self.args, "batch_size", 1))
-        if self._handle is not None and self._handle.native and self._handle.comm_gen != SharedComm.generation:
+        if SharedComm.stale(self._handle):
             self._handle = None   # its communicator was freed (SharedComm.free detached it): rebuild and re-attach
         if self._handle is None or self._handle_key[0] < need_b or self._handle_key[1] < T:
             cfg = make_coma_config(self.args, self.mac.agent.input_dim, need_b, T)
@@ -220,11 +220,11 @@ class COMALearner:
         steps = int(round(st[9]))
         if steps < 0:
             # the library put the critic back to its pre-train version and skipped the actor update: the learner's
-            # state is this call's starting state (no step counted), so a retry or MQ_COMA_CHAIN=0 can follow. Under
+            # state is this call's starting state (no step counted), so a retry or MQ_PLAN=coma_chain=0 can follow. Under
             # data parallelism the failure word travels with the agent gradient's all-reduce, so every rank rolled
             # back and raises here together and a retry keeps the ranks' collective sequence in step
             raise _lib.MQError("COMA critic chain: a workgroup hand-off timed out; this train() was rolled back "
-                               "(critic and agent unchanged; MQ_COMA_CHAIN=0 selects the three-launch critic)")
+                               "(critic and agent unchanged; MQ_PLAN=coma_chain=0 selects the three-launch critic)")
         self.critic_training_steps += steps
         self._steps += 1
         for p in self.agent_params:

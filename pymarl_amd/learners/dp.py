@@ -75,13 +75,16 @@ def _t_len(batch):
 # fields whose sampled rows are digested: what the loss reads (q_learner.py:39-44, 58-86; coma_learner.py:32-46)
 DIGEST_FIELDS = ("reward", "actions", "terminated", "filled", "avail_actions", "obs", "state")
 _MIX = -7046029254386353131   # 0x9E3779B97F4A7C15 as int64 (golden-ratio multiplier); products wrap mod 2^64
+DIGEST_CHUNK = 1 << 22        # elements per hashing pass (5 int64 temporaries of 32 MB each)
 
 
 def content_digest(batch):
     """64-bit digest of the CONTENTS of the sampled transitions (the fields the learner reads, DIGEST_FIELDS), computed
     where the batch lives (device kernels for a GPU replay, one host read-back). Every element's bit pattern is mixed
     with its position and the sum wraps in int64, so the result does not depend on the summation order: two ranks get
-    the same digest exactly when their sampled rows are bitwise equal (up to hash collisions)."""
+    the same digest exactly when their sampled rows are bitwise equal (up to hash collisions). Each field is hashed
+    in chunks of DIGEST_CHUNK elements, so the int64 temporaries stay a few hundred MB whatever the batch size; the
+    chunk sums add up modulo 2^64 to the whole field's sum."""
     acc = 0
     for k in DIGEST_FIELDS:
         try:
@@ -90,11 +93,15 @@ def content_digest(batch):
             continue
         if v.dtype == torch.float32:
             v = v.contiguous().view(torch.int32)
-        v = v.reshape(-1).to(torch.int64)
-        pos = torch.arange(1, v.numel() + 1, dtype=torch.int64, device=v.device)
-        x = (v + pos) * _MIX
-        x = x ^ (x >> 29)          # arithmetic shift: deterministic for negative values too
-        acc = (acc * 31 + int((x * _MIX).sum().item())) & 0xFFFFFFFFFFFFFFFF
+        v = v.reshape(-1)
+        s = 0
+        for lo in range(0, v.numel(), DIGEST_CHUNK):
+            c = v[lo:lo + DIGEST_CHUNK].to(torch.int64)
+            pos = torch.arange(lo + 1, lo + c.numel() + 1, dtype=torch.int64, device=c.device)
+            x = (c + pos) * _MIX
+            x = x ^ (x >> 29)          # arithmetic shift: deterministic for negative values too
+            s += int((x * _MIX).sum().item())
+        acc = (acc * 31 + s) & 0xFFFFFFFFFFFFFFFF
     return acc
 
 
@@ -210,9 +217,18 @@ class SharedComm:
         handle.comm_gen = cls.generation
 
     @classmethod
+    def stale(cls, handle):
+        """True when `handle` borrowed a communicator that has since been freed (free() detached it and moved the
+        generation on). Independent of `handle.native`, which free() clears: the learner must rebuild such a handle
+        so the next train() re-attaches, instead of training on with no cross-rank sum."""
+        gen = getattr(handle, "comm_gen", None) if handle is not None else None
+        return gen is not None and gen != cls.generation
+
+    @classmethod
     def free(cls):
         """Release the communicator (call after the last train() and before destroy_process_group). Every handle
-        that still borrows it is detached first and falls back to `native = False` until it re-attaches."""
+        that still borrows it is detached first and falls back to `native = False`; the learner rebuilds it on its
+        next train() (stale()), which re-attaches a new communicator."""
         if cls._comm is not None:
             from .. import _lib
             for ref, detach in cls._borrowers:

@@ -20,7 +20,6 @@ from __future__ import annotations
 
 import copy
 import ctypes
-import os
 
 import numpy as np
 
@@ -81,9 +80,11 @@ def _field_view(t, dtype):
     return t, t.stride(0) // max(1, inner)
 
 
-def replay_view(batch):
+def replay_view(batch, avail_bits=True):
     """MQReplay for an EpisodeBatch (episode-major storage) or a SampledBatch (storage + device ids).
-    Returns (struct, keepalive) — keep the second alive until the kernels that read it have been queued."""
+    Returns (struct, keepalive) — keep the second alive until the kernels that read it have been queued.
+    avail_bits: hand the kernels the buffer's avail bitmask (ReplayBuffer.avail_bits_current: rebuilt first if the
+    storage was written behind its back), else they read the int32 avail_actions rows."""
     keep = []
     rep = _lib.MQReplay()
     if is_replay_view(batch):
@@ -109,8 +110,9 @@ def replay_view(batch):
             if t.dtype != dt or not t.is_contiguous():
                 raise _lib.MQError("replay field {} must be a contiguous {} tensor".format(k, dt))
             tensors[k] = t
-        bits = getattr(batch.source, "avail_bits", None)
-        if bits is not None and os.environ.get("MQ_AVAIL_BITS", "1") != "0":   # =0: A/B switch, read avail_actions
+        cur = getattr(batch.source, "avail_bits_current", None)
+        bits = cur() if (avail_bits and cur is not None) else None
+        if bits is not None:
             keep.append(bits)
             rep.avail_bits = bits.data_ptr()
     else:
@@ -162,6 +164,9 @@ class QLearner:
         # when to check that the ranks passed the same global sample (ids AND contents): a call-count schedule, the
         # same on every rank (dp.DPCheck: "first", "always", "off" or every N calls, default 100)
         self.dp_check = DPCheck(getattr(args, "learner_dp_check", None))
+        # the mixer's double-Q selection reads the replay buffer's avail bitmask (False: the int32 avail_actions rows;
+        # bitwise the same result, test_avail_bits_bitwise)
+        self.use_avail_bits = bool(getattr(args, "learner_avail_bits", True))
 
         # flat device buffers: [agent params | mixer params] for online and target nets (MQ_P_* order)
         self._mods = [m for m in (self.mac.agent, self.mixer) if m is not None and len(list(m.parameters()))]
@@ -225,7 +230,7 @@ class QLearner:
         world = dp_world()[1] if self._dp_active() else 1
         need_b = max(batch.batch_size, -(-getattr(self.args, "batch_size", 1) // world))
         key = (need_b, T)
-        if self._handle is not None and self._handle.native and self._handle.comm_gen != SharedComm.generation:
+        if SharedComm.stale(self._handle):
             self._handle = None   # its communicator was freed (SharedComm.free detached it): rebuild and re-attach
         if self._handle is None or self._handle_key[0] < need_b or self._handle_key[1] < T:
             cfg = make_config(self.args, MIXER_IDS[self.args.mixer], input_dim=self.mac.agent.input_dim,
@@ -259,7 +264,7 @@ class QLearner:
         if want != h.dp_on:
             _lib.check(h.lib.mq_set_data_parallel(h.h, int(want)))
             h.dp_on = want
-        rep, keep = replay_view(batch)
+        rep, keep = replay_view(batch, self.use_avail_bits)
         lib, s = h.lib, _lib.stream_ptr()
         if dp and not h.native:
             _lib.check(lib.mq_forward_backward(h.h, ctypes.byref(rep), s))

@@ -12,9 +12,9 @@ from tests.gpu_helpers import build, flat_grads  # noqa: E402
 
 def run(case, unfused):
     if unfused:
-        os.environ["MQ_UNFUSED_FWD"] = "1"
+        os.environ["MQ_PLAN"] = "unfused_fwd"
     else:
-        os.environ.pop("MQ_UNFUSED_FWD", None)
+        os.environ.pop("MQ_PLAN", None)
     args, buf, mac, learner, logger = build(case)
     np.random.seed(case.sampler_seed)
     batch = buf.sample(case.B)

@@ -1,15 +1,16 @@
-"""Decode the row-pair forward's stamps (MQ_PAIR_STAMP=<file>, gru_fwd_pair.hpp STAMP) of the last train(), cycles
+"""Decode the row-pair forward's stamps (MQ_DIAG=pair_stamp=<file>, gru_fwd_pair.hpp STAMP) of the last train(), cycles
 (s_memtime ticks) from kernel entry: prologue, recurrence loop, epilogue; per-step cost inside a chunk and across a
 chunk boundary; producers' slack at each chunk barrier. Usage: python scripts/pair_stamps.py <file> <Tp>"""
 import sys
 import numpy as np
 
-PST = 16 + 2 * 512
+PSH = 32
+PST = PSH + 2 * 512
 path, Tp = sys.argv[1], int(sys.argv[2])
 a = np.fromfile(path, dtype=np.uint32)[-8 * PST:].reshape(8, PST).astype(np.int64)
 rel = (a - a[:, :1]) % (1 << 32)
 entry, lstart, lend, pro, kend = (rel[:, i] for i in range(5))
-steps = rel[:, 16:16 + Tp]
+steps = rel[:, PSH:PSH + Tp]
 print("per block (mean of 8): recurrence loop starts at %.0f, producers' prologue done at %.0f, loop ends at %.0f,"
       " kernel ends at %.0f cycles" % (lstart.mean(), pro.mean(), lend.mean(), kend.mean()))
 per = np.diff(steps, axis=1)
@@ -17,11 +18,14 @@ t = np.arange(1, Tp)
 ins = (t % 16) != 0
 print("producers: loads issued %.0f, landed %.0f, X1(0..1) %.0f, GI(0) %.0f; recurrence W_hh landed %.0f" %
       tuple(rel[:, i].mean() for i in (5, 6, 7, 8, 9)))
+print("producer 0's prologue: S1 %.0f, gather issued %.0f, W1 / W2 issued %.0f, S2 %.0f, W_ih staged %.0f, xin(0) %.0f, "
+      "S3 %.0f, W_ih picked + xin(1) %.0f, S4 %.0f, X1(0..1) %.0f, S5 %.0f, GI(0) %.0f" %
+      tuple(rel[:, i].mean() for i in (16, 17, 5, 18, 6, 19, 20, 3, 21, 7, 22, 8)))
 print("hypernet waves (HYP=2): tiles done in the S3/S4/S5/chunk-0 intervals %s, exit %.0f" % ([round(rel[:, 11 + i].mean()) for i in range(4)], rel[:, 15].mean()))
 print("step cycles inside a chunk: mean %.0f, median %.0f; first step of a chunk: mean %.0f; step 0 ends %.0f after "
       "the loop start" % (per[:, ins].mean(), np.median(per[:, ins]), per[:, ~ins].mean(),
                           (steps[:, 0] - lstart).mean()))
 last = np.arange(15, Tp, 16)
-arr = rel[:, 16 + 512 + last]
+arr = rel[:, PSH + 512 + last]
 print("producers' chunk-barrier arrival - recurrence's chunk end (cycles, + = producers late):",
       np.round((arr - steps[:, last]).mean(0)).astype(int).tolist())

@@ -111,3 +111,28 @@ def build_coma(case, device="cuda", **over):
     learner.critic.load_state_dict(cd)
     learner.target_critic.load_state_dict(cd)
     return args, buf, mac, learner, logger
+
+
+# The library's two switch variables (pymarl_amd/csrc/switches.hpp): MQ_PLAN for plan overrides, MQ_DIAG for
+# diagnostics and test hooks, each a comma-separated list of `key` / `key=value` items.
+DIAG_KEYS = ("pair_stamp", "hyp_sched", "coma_trace", "coma_fault")
+
+
+def switch_value(env, key, value):
+    """`env`'s MQ_PLAN / MQ_DIAG string with item `key` set (value True: a bare key; str / int: key=value) or
+    removed (value None)."""
+    var = "MQ_DIAG" if key in DIAG_KEYS else "MQ_PLAN"
+    items = [i for i in env.get(var, "").split(",") if i and i.split("=", 1)[0] != key]
+    if value is not None:
+        items.append(key if value is True else "{}={}".format(key, value))
+    return var, ",".join(items)
+
+
+def set_switch(monkeypatch, key, value=True):
+    """monkeypatch-scoped set_switch: restored after the test."""
+    import os
+    var, v = switch_value(os.environ, key, value)
+    if v:
+        monkeypatch.setenv(var, v)
+    else:
+        monkeypatch.delenv(var, raising=False)

@@ -239,3 +239,60 @@ def test_shared_comm_free_detaches_borrowers():
     SharedComm.free()
     assert lib.calls == [("mq", 16), ("mc", 32)]
     assert not a.native and not b.native and SharedComm._comm is None and SharedComm.generation == gen + 1
+
+
+def test_learner_rebuilds_handle_after_shared_comm_free(monkeypatch):
+    """after SharedComm.free() detached a borrowed communicator, the learner's next _get_handle must
+    build a new handle that borrows the new communicator (data parallelism still on), not train on with the detached
+    one. free() clears `native`, so the rebuild must not depend on it (SharedComm.stale keys on the generation)."""
+    import ctypes
+    from types import SimpleNamespace as SN
+    from pymarl_amd import _lib
+    from pymarl_amd.learners import q_learner as ql
+    from pymarl_amd.learners.dp import SharedComm
+
+    class _Lib:
+        def mq_bind(self, *a):
+            return 0
+
+        def mq_comm_detach(self, h):
+            return 0
+
+        def mq_comm_free(self, c):
+            return 0
+
+    built = []
+
+    class _FakeHandle:
+        def __init__(self, cfg):
+            self.lib, self.h, self.n_params = _Lib(), ctypes.c_void_p(len(built) + 1), 10
+            built.append(self)
+
+    lent = []
+
+    def _lend(handle, use, detach, device):
+        import weakref
+        SharedComm._comm = ctypes.c_void_p(None)
+        SharedComm._borrowers.append((weakref.ref(handle), detach))
+        handle.native, handle.comm_gen = True, SharedComm.generation
+        lent.append(handle)
+
+    monkeypatch.setattr(ql._lib, "Handle", _FakeHandle)
+    monkeypatch.setattr(ql, "native_comm_wanted", lambda dev: True)
+    monkeypatch.setattr(SharedComm, "lend", staticmethod(_lend))
+    monkeypatch.setattr(_lib, "load", lambda: _Lib())
+    monkeypatch.setattr(SharedComm, "_borrowers", [])
+    args = SN(batch_size=4, n_agents=2, n_actions=3, obs_shape=5, state_shape=4, rnn_hidden_dim=64,
+              mixing_embed_dim=8, mixer="qmix", obs_last_action=True, obs_agent_id=True)
+    fake = SN(args=args, mac=SN(agent=SN(input_dim=10)), _online=th.zeros(11), _target=th.zeros(11),
+              _grad=th.zeros(11), _sq=th.zeros(10), _stats=th.zeros(8), n_params=10, _handle=None,
+              _handle_key=None, _dp_active=lambda: True)
+    monkeypatch.setattr(ql, "dp_world", lambda: (0, 2))
+    batch = SN(batch_size=2, max_seq_length=6)
+    h1 = ql.QLearner._get_handle(fake, batch)
+    assert ql.QLearner._get_handle(fake, batch) is h1 and h1.native
+    SharedComm.free()
+    assert not h1.native and SharedComm.stale(h1)
+    h2 = ql.QLearner._get_handle(fake, batch)
+    assert h2 is not h1 and h2.native and not SharedComm.stale(h2) and lent == [h1, h2]
+    assert not SharedComm.stale(None) and not SharedComm.stale(SN(native=False))

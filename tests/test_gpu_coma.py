@@ -15,6 +15,7 @@ import pytest
 import torch as th
 
 from tests.golden_utils import COMA_STATS, ComaCase
+from tests.gpu_helpers import set_switch
 
 pytestmark = pytest.mark.gpu
 
@@ -147,7 +148,7 @@ def test_mac_pi_logits_policy(coma_cases):
 
 @pytest.mark.parametrize("name", ["coma_tiny_masked", "coma_cfg5"])
 def test_coma_chain_matches_three_launch(coma_cases, name, monkeypatch):
-    """The persistent critic chain (coma_chain.hpp, default) against the three-launch path (MQ_COMA_CHAIN=0) from
+    """The persistent critic chain (coma_chain.hpp, default) against the three-launch path (MQ_PLAN coma_chain=0) from
     the same state on the same batches: same products, other fixed summation orders for the bias gradients and
     the norm, so agreement to float rounding amplified along the T-step chain (tolerances as the oracle's)."""
     from oracle.coma_np import OracleCOMALearner
@@ -156,10 +157,7 @@ def test_coma_chain_matches_three_launch(coma_cases, name, monkeypatch):
     o = OracleCOMALearner(c.agent_params, c.critic_params, c.cfg())
     runs = {}
     for path, env in (("chain", None), ("three_launch", "0")):
-        if env is None:
-            monkeypatch.delenv("MQ_COMA_CHAIN", raising=False)
-        else:
-            monkeypatch.setenv("MQ_COMA_CHAIN", env)
+        set_switch(monkeypatch, "coma_chain", env)
         args, buf, mac, learner, logger = build_coma(c)
         np.random.seed(c.sampler_seed)
         out = []
@@ -192,10 +190,7 @@ def test_coma_skipped_critic_steps(path, env, monkeypatch):
     oracle through both critic paths; critic_steps counts the live steps only."""
     from oracle.coma_np import OracleCOMALearner
     from tests.gpu_helpers import build_coma
-    if env is None:
-        monkeypatch.delenv("MQ_COMA_CHAIN", raising=False)
-    else:
-        monkeypatch.setenv("MQ_COMA_CHAIN", env)
+    set_switch(monkeypatch, "coma_chain", env)
     c = ComaCase("coma_tiny_masked")
     for h in (2, 5):
         c.data["filled"][:, h] = 0
@@ -225,14 +220,14 @@ def test_coma_skipped_critic_steps(path, env, monkeypatch):
 
 
 def test_coma_chain_failure_is_loud(monkeypatch):
-    """A persistent-chain workgroup that stops flagging (MQ_COMA_CHAIN_FAULT test hook) makes every workgroup leave
+    """A persistent-chain workgroup that stops flagging (MQ_DIAG coma_fault test hook) makes every workgroup leave
     within the bounded spin: the launch ends, the stats come out NaN with critic_steps = -1 and train() raises.
     The failed train() is rolled back: critic params / square_avg are restored and the actor update is skipped, so
     every parameter and optimiser buffer is bitwise its pre-train value, and the next train() equals a clean
     learner's first train() on the same batch bit for bit."""
     from tests.gpu_helpers import build_coma
     from pymarl_amd._lib import MQError
-    monkeypatch.delenv("MQ_COMA_CHAIN", raising=False)
+    set_switch(monkeypatch, "coma_chain", None)
     c = get({}, "coma_tiny")
     args, buf, mac, learner, logger = build_coma(c)
     np.random.seed(c.sampler_seed)
@@ -241,7 +236,7 @@ def test_coma_chain_failure_is_loud(monkeypatch):
     mac.action_selector.epsilon = c.epsilon[0]
     snap = lambda l: [t.cpu().numpy().copy() for t in (l._critic, l._csq, l._agent, l._asq, l._tcritic)]  # noqa
     before = snap(learner)
-    monkeypatch.setenv("MQ_COMA_CHAIN_FAULT", "1")
+    set_switch(monkeypatch, "coma_fault", "1")
     with pytest.raises(MQError):
         learner.train(batch, 1000, 0)
     assert learner.critic_path() == "chain"
@@ -249,7 +244,7 @@ def test_coma_chain_failure_is_loud(monkeypatch):
     for a, b in zip(before, snap(learner)):
         assert np.array_equal(a, b)
     assert learner.critic_training_steps == 0
-    monkeypatch.delenv("MQ_COMA_CHAIN_FAULT")
+    set_switch(monkeypatch, "coma_fault", None)
     learner.train(batch, 2000, 8)
     st = learner.last_stats()
     assert st["critic_steps"] > 0 and np.isfinite(st["critic_loss"])
@@ -266,7 +261,7 @@ def test_coma_chain_bitwise_deterministic(coma_cases, monkeypatch):
     the same state on the same batch give bitwise-identical critic parameters, square_avg and stats."""
     from oracle.coma_np import OracleCOMALearner
     from tests.gpu_helpers import build_coma
-    monkeypatch.delenv("MQ_COMA_CHAIN", raising=False)
+    set_switch(monkeypatch, "coma_chain", None)
     c = get(coma_cases, "coma_cfg5")
     args, buf, mac, learner, logger = build_coma(c)
     o = OracleCOMALearner(c.agent_params, c.critic_params, c.cfg())

@@ -191,7 +191,7 @@ def test_two_rank_coma_dp_equals_single_process(tmp_path, name, steps, mode):
     assert np.abs(dp["agent"][-1] - ref["agent"][-1]).max() <= 20 * 5e-4
 
 
-# A critic-chain timeout on ONE rank of a replicated data-parallel COMA (the MQ_COMA_CHAIN_FAULT test hook, set on
+# A critic-chain timeout on ONE rank of a replicated data-parallel COMA (the MQ_DIAG coma_fault test hook, set on
 # rank 1 only): the failure word rides in the agent gradient's all-reduce, so BOTH ranks restore the critic, skip the
 # actor update and raise, and both learners are bitwise in their pre-train state (a one-rank rollback let
 # the ranks' parameters diverge).
@@ -215,13 +215,13 @@ def _coma_fault_worker(rank, world, port, out_path):
         before = [t.detach().cpu().numpy().copy() for t in (learner._critic, learner._csq, learner._agent,
                                                               learner._asq)]
         if rank == 1:
-            os.environ["MQ_COMA_CHAIN_FAULT"] = "1"
+            os.environ["MQ_DIAG"] = "coma_fault=1"
         raised = 0
         try:
             learner.train(gb, 2000, 8)
         except _lib.MQError:
             raised = 1
-        os.environ.pop("MQ_COMA_CHAIN_FAULT", None)
+        os.environ.pop("MQ_DIAG", None)
         after = [t.detach().cpu().numpy() for t in (learner._critic, learner._csq, learner._agent, learner._asq)]
         same = int(all(np.array_equal(a, b) for a, b in zip(before, after)))
         learner.train(gb, 3000, 16)   # and the ranks stay in step afterwards

@@ -12,6 +12,7 @@ import pytest
 import torch as th
 
 from tests.golden_utils import COMA_STATS, Case, ComaCase
+from tests.gpu_helpers import set_switch
 
 pytestmark = pytest.mark.gpu
 
@@ -60,7 +61,7 @@ def test_qlearner_step_over_native_rccl(monkeypatch):
 def test_coma_step_over_native_rccl(monkeypatch):
     from tests.gpu_helpers import build_coma
     monkeypatch.setenv("NCCL_SOCKET_IFNAME", "lo")
-    monkeypatch.setenv("MQ_COMA_CHAIN", "0")   # the reference path for the comparison: three launches, no exchange
+    set_switch(monkeypatch, "coma_chain", "0")   # the reference path for the comparison: three launches, no exchange
     c = ComaCase("coma_tiny")
     runs = []
     for native in (True, False):
@@ -114,7 +115,7 @@ def test_caller_owned_communicator_shared_by_two_learners(monkeypatch):
                 assert h.lib.mq_comm_detach(h.h) == 0   # borrowed: the communicator stays alive
         assert _rel(out[0], out[1]) < 1e-6
 
-        monkeypatch.setenv("MQ_COMA_CHAIN", "0")
+        set_switch(monkeypatch, "coma_chain", "0")
         c = ComaCase("coma_tiny")
         runs = []
         for use in (True, False):
@@ -149,7 +150,7 @@ def test_coma_replicated_critic_world1(monkeypatch):
     all-reduce is the identity (agent parameters equal to rounding: the norm is recomputed from the summed buffer)."""
     from tests.gpu_helpers import build_coma
     monkeypatch.setenv("NCCL_SOCKET_IFNAME", "lo")
-    monkeypatch.delenv("MQ_COMA_CHAIN", raising=False)
+    set_switch(monkeypatch, "coma_chain", None)
     c = ComaCase("coma_cfg5")
     runs = []
     for repl in (True, False):

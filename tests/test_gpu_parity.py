@@ -28,6 +28,7 @@ import pytest
 import torch as th
 
 from tests.golden_utils import Case
+from tests.gpu_helpers import set_switch
 
 pytestmark = pytest.mark.gpu
 
@@ -234,8 +235,8 @@ def test_wide_batch_paths_vs_reference(cases, name):
     run_case(get_case(cases, name), check_full=False, plan=WIDE_PLANS[name])
 
 
-# The row-batched GEMM + recurrence path the row tiles replaced (MQ_ROW_TILES=0): gru_fwd_kernel<RW> (RW = 2 / 4 / 8
-# rows per workgroup) and gru_bwd_kernel<2>, still the path for shapes past the tiles' limits, pinned to the same
+# The row-batched GEMM + recurrence path the row tiles replaced (MQ_PLAN row_tiles=0): gru_fwd_kernel<RW>
+# (RW = 2 / 4 / 8 rows per workgroup) and gru_bwd_kernel<2>, still the path for shapes past the tiles' limits, pinned to the same
 # reference goldens.
 RW_PLANS = {
     "rw2_qmix": dict(rows=576, tiles=0, fused_fwd=0, rw_fwd=2, fused_bwd=0, rw_bwd=2, inline_ids=1, hyper="ws"),
@@ -246,11 +247,11 @@ RW_PLANS = {
 
 @pytest.mark.parametrize("name", sorted(RW_PLANS))
 def test_row_batched_paths_vs_reference(cases, name, monkeypatch):
-    monkeypatch.setenv("MQ_ROW_TILES", "0")
+    set_switch(monkeypatch, "row_tiles", "0")
     run_case(get_case(cases, name), check_full=False, plan=RW_PLANS[name])
 
 
-# The row-tile path forced onto every shape it takes (MQ_ROW_TILES=1), teacher-forced against the oracle: partial
+# The row-tile path forced onto every shape it takes (MQ_PLAN row_tiles=1), teacher-forced against the oracle: partial
 # tiles (R not a multiple of 16 / 32), ragged episodes, VDN / QMIX / IQL, the obs_last_action / obs_agent_id = False
 # branches, configs[2]'s shape at B = 4 and configs[3]'s shard.
 @pytest.mark.parametrize("name,steps", [
@@ -258,7 +259,7 @@ def test_row_batched_paths_vs_reference(cases, name, monkeypatch):
     ("tiny_vdn_noid", 3), ("cfg2_qmix", 3), ("cfg2_qmix_ragged", 3), ("cfg3_vdn", 3), ("cfg3_qmix", 2),
     ("cfg4_qmix", 2), ("cfg1_qmix", 3)])
 def test_row_tiles_teacher_forced(cases, name, steps, monkeypatch):
-    monkeypatch.setenv("MQ_ROW_TILES", "1")
+    set_switch(monkeypatch, "row_tiles", "1")
     learner = run_teacher_forced(get_case(cases, name), steps, False, monkeypatch)
     assert learner.last_plan()["tiles"] == 1
 
@@ -326,7 +327,7 @@ def set_state_from_oracle(learner, o):
         learner._sq.copy_(th.from_numpy(o.flat("sq")))
 
 
-UNFUSED_ENV = ("MQ_UNFUSED_FWD", "MQ_UNFUSED_BWD")
+UNFUSED_KEYS = ("unfused_fwd", "unfused_bwd")   # MQ_PLAN items (pymarl_amd/csrc/switches.hpp)
 
 
 @pytest.mark.parametrize("name,steps,unfused", [
@@ -356,20 +357,10 @@ def test_teacher_forced_steps(cases, name, steps, unfused, monkeypatch):
 def test_forward_pair_switch_teacher_forced(cases, name, steps, pair, monkeypatch):
     """Both one-wave agent forwards teacher-forced against the oracle: the row-pair kernel (gru_fwd_pair.hpp, both nets
     of a row per workgroup; the default when the rows fit the CUs) and the one-row-net kernel it replaced there
-    (MQ_FWD_PAIR=0; still the forward past one wave of rows, e.g. configs[3]'s shard)."""
-    monkeypatch.setenv("MQ_FWD_PAIR", pair)
+    (MQ_PLAN fwd_pair=0; still the forward past one wave of rows, e.g. configs[3]'s shard)."""
+    set_switch(monkeypatch, "fwd_pair", pair)
     learner = run_teacher_forced(get_case(cases, name), steps, False, monkeypatch)
     assert learner.last_plan()["fused_fwd"] == (2 if pair == "1" else 1)
-
-
-@pytest.mark.parametrize("name,steps", [("cfg2_qmix", 3), ("cfg2_qmix_ragged", 3), ("tiny_vdn", 3), ("tiny_iql", 3),
-                                        ("tiny_qmix_bare", 3), ("cfg1_qmix", 3), ("cfg2_vdn", 2), ("cfg1_vdn", 3)])
-def test_bwd_pair_teacher_forced(cases, name, steps, monkeypatch):
-    """The one-chain-wave BPTT (gru_bwd_pair.hpp, MQ_BWD_PAIR=1: a row's chain on one wave, lane = unit, the weight
-    gradients on the other SIMDs) teacher-forced against the oracle: stats, gradients and the RMSprop step."""
-    monkeypatch.setenv("MQ_BWD_PAIR", "1")
-    learner = run_teacher_forced(get_case(cases, name), steps, False, monkeypatch)
-    assert learner.last_plan()["fused_bwd"] == 2
 
 
 @pytest.mark.parametrize("name,steps,flow", [
@@ -406,11 +397,8 @@ def run_teacher_forced(case, steps, unfused, monkeypatch, flow="view", huber=0.0
     from oracle.qlearner_np import OracleQLearner
     from tests.gpu_helpers import build, flat_grads, flat_params, rel
     name = case.name
-    for k in UNFUSED_ENV:   # read once, at handle creation (mq_create)
-        if unfused:
-            monkeypatch.setenv(k, "1")
-        else:
-            monkeypatch.delenv(k, raising=False)
+    for k in UNFUSED_KEYS:   # read once, at handle creation (mq_create)
+        set_switch(monkeypatch, k, True if unfused else None)
     over = {"td_loss": "huber", "huber_delta": huber} if huber else {}
     args, buf, mac, learner, logger = build(case, buffer_device="cpu" if flow == "cpu_to" else None, **over)
     o = OracleQLearner(case.agent_params, case.mixer_params, dict(case.cfg(), huber_delta=huber))
@@ -467,7 +455,7 @@ def run_teacher_forced(case, steps, unfused, monkeypatch, flow="view", huber=0.0
     if flow == "dense_slice":   # every truncated batch is read in place with t_stride = T + 1 > t_len
         assert strided == truncated, (strided, truncated)
         assert case.name != "cfg1_qmix" or strided == steps
-    tag = "_tiles" if os.environ.get("MQ_ROW_TILES") == "1" else ""
+    tag = "_tiles" if "row_tiles=1" in os.environ.get("MQ_PLAN", "").split(",") else ""
     write_record("teacher" + ("_unfused" if unfused else "") + tag + ("_huber" if huber else "")
                  + ("" if flow == "view" else "_" + flow), name, rec)
     return learner
@@ -502,16 +490,17 @@ def test_data_parallel_norm_path_single_rank(cases):
 
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg4_qmix", "cfg1_qmix", "tiny_qmix_full", "cfg2_qmix_ragged"])
 def test_hyper_in_forward_grid_bitwise(cases, name, monkeypatch):
-    """The QMIX hypernet as workgroups appended to the fused forward's grid (MQ_HYP_IN_FWD=1; the default for shards
-    past two row-nets per CU, e.g. cfg4) equals hyper_ws_kernel launched after the forward (MQ_HYP_IN_FWD=0) bitwise:
+    """The QMIX hypernet as workgroups appended to the fused forward's grid (MQ_PLAN hyp_in_fwd=1; the default for
+    shards past two row-nets per CU, e.g. cfg4) equals hyper_ws_kernel launched after the forward (MQ_PLAN
+    hyp_in_fwd=0) bitwise:
     parameters, gradients, square_avg and stats over up to four steps, ragged M (cfg1: M = 480, tiny) and the
     two-wave forward of configs[3]'s shard (cfg4) included."""
     from tests.gpu_helpers import build, flat_grads, flat_params
     case = get_case(cases, name)
     outs = []
-    monkeypatch.setenv("MQ_FWD_PAIR", "0")   # both arms on the one-row-net forward (the pair kernel has no HYP grid)
+    set_switch(monkeypatch, "fwd_pair", "0")   # both arms on the one-row-net forward (the pair kernel has no HYP grid)
     for inf in ("1", "0"):
-        monkeypatch.setenv("MQ_HYP_IN_FWD", inf)
+        set_switch(monkeypatch, "hyp_in_fwd", inf)
         args, buf, mac, learner, logger = build(case)
         np.random.seed(case.sampler_seed)
         for k in range(min(4, len(case.episodes))):
@@ -529,22 +518,22 @@ def test_hyper_in_forward_grid_bitwise(cases, name, monkeypatch):
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg1_qmix", "tiny_qmix_full", "cfg2_qmix_ragged"])
 def test_pair_hyper_epilogue_bitwise(cases, name, monkeypatch):
     """The QMIX hypernet inside the row-pair forward — on waves 4 / 5 during the T loop (the default when every
-    hypernet block has a workgroup) or as the kernel's epilogue (MQ_PAIR_HYP_EPI=1, and the default otherwise) —
-    equals hyper_ws_kernel launched after the forward (MQ_HYP_IN_FWD=0) bitwise: parameters, gradients, square_avg
+    hypernet block has a workgroup) or as the kernel's epilogue (MQ_PLAN pair_hyp_epi, and the default otherwise) —
+    equals hyper_ws_kernel launched after the forward (MQ_PLAN hyp_in_fwd=0) bitwise: parameters, gradients, square_avg
     and stats over up to four steps, ragged M included."""
     from tests.gpu_helpers import build, flat_grads, flat_params
     case = get_case(cases, name)
     outs = []
-    monkeypatch.setenv("MQ_FWD_PAIR", "1")
+    set_switch(monkeypatch, "fwd_pair", "1")
     for inf, epi in ((None, False), (None, True), ("0", False)):
         if epi:
-            monkeypatch.setenv("MQ_PAIR_HYP_EPI", "1")
+            set_switch(monkeypatch, "pair_hyp_epi")
         else:
-            monkeypatch.delenv("MQ_PAIR_HYP_EPI", raising=False)
+            set_switch(monkeypatch, "pair_hyp_epi", None)
         if inf is None:
-            monkeypatch.delenv("MQ_HYP_IN_FWD", raising=False)
+            set_switch(monkeypatch, "hyp_in_fwd", None)
         else:
-            monkeypatch.setenv("MQ_HYP_IN_FWD", inf)
+            set_switch(monkeypatch, "hyp_in_fwd", inf)
         args, buf, mac, learner, logger = build(case)
         np.random.seed(case.sampler_seed)
         for k in range(min(4, len(case.episodes))):
@@ -563,15 +552,15 @@ def test_pair_hyper_epilogue_bitwise(cases, name, monkeypatch):
 @pytest.mark.parametrize("name", ["cfg3_vdn", "cfg3_qmix", "cfg3_vdn_b128"])
 def test_mix_stream_bitwise(cases, name, monkeypatch):
     """configs[2]'s mixer with the selection rows staged by the workgroup (mix_kernel<true>, the default where
-    n * A <= 1024) equals the per-lane generic form (MQ_MIX_GENERIC=1) bitwise, double-Q argmax included."""
+    n * A <= 1024) equals the per-lane generic form (MQ_PLAN mix_generic) bitwise, double-Q argmax included."""
     from tests.gpu_helpers import build, flat_grads, flat_params
     case = get_case(cases, name)
     outs = []
     for gen in ("0", "1"):
         if gen == "1":
-            monkeypatch.setenv("MQ_MIX_GENERIC", "1")
+            set_switch(monkeypatch, "mix_generic")
         else:
-            monkeypatch.delenv("MQ_MIX_GENERIC", raising=False)
+            set_switch(monkeypatch, "mix_generic", None)
         args, buf, mac, learner, logger = build(case)
         np.random.seed(case.sampler_seed)
         for k in range(min(2, len(case.episodes))):
@@ -589,16 +578,16 @@ def test_mix_stream_bitwise(cases, name, monkeypatch):
                                           ("tiny_qmix_full", False), ("cfg3_qmix", True)])
 def test_avail_bits_bitwise(cases, name, generic, monkeypatch):
     """The mixer's double-Q selection reading the replay buffer's avail bitmask (mq_replay.avail_bits, the default
-    for buffer views) equals it reading avail_actions (MQ_AVAIL_BITS=0) bitwise, in the staged (stream), per-lane
-    (MQ_MIX_GENERIC=1) and fast mixers; the chosen argmax actions too."""
+    for buffer views) equals it reading avail_actions (learner.use_avail_bits = False) bitwise, in the staged
+    (stream), per-lane (MQ_PLAN mix_generic) and fast mixers; the chosen argmax actions too."""
     from tests.gpu_helpers import build, flat_grads, flat_params
     case = get_case(cases, name)
     if generic:
-        monkeypatch.setenv("MQ_MIX_GENERIC", "1")
+        set_switch(monkeypatch, "mix_generic")
     outs = []
-    for bits in ("1", "0"):
-        monkeypatch.setenv("MQ_AVAIL_BITS", bits)
+    for bits in (True, False):
         args, buf, mac, learner, logger = build(case)
+        learner.use_avail_bits = bits
         assert buf.avail_bits is not None
         np.random.seed(case.sampler_seed)
         acts = []
@@ -617,14 +606,14 @@ def test_avail_bits_bitwise(cases, name, generic, monkeypatch):
 
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg4_qmix", "cfg1_qmix", "tiny_qmix_full"])
 def test_dwh_in_bptt_grid_bitwise(cases, name, monkeypatch):
-    """dW_hyper's tiles appended to the fused BPTT's grid (MQ_DWH_IN_BWD=1; the default for shards past the CU count,
-    e.g. cfg4) equal dW_hyper in the reduction's launch (MQ_DWH_IN_BWD=0) bitwise: parameters, gradients,
+    """dW_hyper's tiles appended to the fused BPTT's grid (MQ_PLAN dwh_in_bwd=1; the default for shards past the CU
+    count, e.g. cfg4) equal dW_hyper in the reduction's launch (MQ_PLAN dwh_in_bwd=0) bitwise: parameters, gradients,
     square_avg and stats over up to four steps."""
     from tests.gpu_helpers import build, flat_grads, flat_params
     case = get_case(cases, name)
     outs = []
     for inb in ("1", "0"):
-        monkeypatch.setenv("MQ_DWH_IN_BWD", inb)
+        set_switch(monkeypatch, "dwh_in_bwd", inb)
         args, buf, mac, learner, logger = build(case)
         np.random.seed(case.sampler_seed)
         for k in range(min(4, len(case.episodes))):

@@ -227,3 +227,33 @@ def test_test_stat_threshold_matches_reference_runners():
         r = cls.__new__(cls)
         r.args, r.batch_size = SN(test_nepisode=n), bs
         assert r.n_test_episodes() == want, (cls.__name__, bs, n)
+
+
+@pytest.mark.parametrize("how", ["index", "view", "replace", "update_after"])
+def test_avail_bits_never_stale_after_direct_writes(how):
+    """The avail bitmask is a derived cache: a write to transition_data["avail_actions"] that bypasses update()
+    (what bench.py and make_golden do, as user code may) must never leave the mixer reading stale bits.
+    ReplayBuffer.avail_bits_current() (what replay_view hands the kernels) notices the storage's write counter moved
+    and rebuilds; a later partial update() after such a write rebuilds everything, not only its own rows."""
+    A = 7
+    rng = np.random.default_rng(1)
+    rb = ReplayBuffer(scheme(A=A), {"agents": 2}, 6, 4)
+    rb.load_arrays({"avail_actions": rng.integers(0, 2, (6, 4, 2, A)).astype(np.int32),
+                    "filled": np.ones((6, 4, 1), np.int64)})
+    assert np.array_equal(rb.avail_bits_current().numpy(), _packed(rb["avail_actions"].numpy()))
+    new = th.from_numpy(rng.integers(0, 2, (6, 4, 2, A)).astype(np.int32))
+    td = rb.data.transition_data
+    if how == "index":
+        td["avail_actions"][2] = new[2]
+    elif how == "view":
+        td["avail_actions"].view(-1, A)[5] = 1 - td["avail_actions"].view(-1, A)[5]
+    elif how == "replace":
+        td["avail_actions"] = new.clone()
+    else:   # a direct write, then a partial update() of OTHER rows
+        td["avail_actions"][0] = new[0]
+        rb.update({"avail_actions": th.ones(2, A, dtype=th.int32)}, bs=4, ts=1)
+        assert np.array_equal(rb.avail_bits.numpy(), _packed(rb["avail_actions"].numpy()))
+    s = rb.sample(3)
+    bits = s.source.avail_bits_current()
+    assert np.array_equal(bits.numpy(), _packed(rb["avail_actions"].numpy()))
+    assert rb.avail_bits_current() is bits   # current now: no second rebuild
