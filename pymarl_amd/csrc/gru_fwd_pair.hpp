@@ -19,36 +19,47 @@
 //      GI of chunk c + 1 = X1 W_ih^T + b_ih (N-tiles 3p .. 3p + 2) -> LDS, read by chunk c + 1's steps
 //      fc1 of chunk c + 2: X1 = relu(XIN W1^T + b1) (N-tile p, W1 in registers)
 //      the inputs of chunk c + 3 staged (obs gathered a chunk earlier, one-hots); chunk c + 4's gather issued.
-// Outputs as gru_fwd_fused_kernel: Q of both nets; X1, XIN, Hs and the gate records of the online net. X1 and GI are
-// bitwise the one-row-net kernel's (same MFMA operand maps and order); h and Q differ by summation order.
+// Outputs as gru_fwd_fused_kernel: Q of both nets; X1, XIN, Hs and the gate records of the online net. fc1 and GI
+// take their K in the order that makes the producers' direct weight loads coalesced (below); X1, h and Q therefore
+// differ from the one-row-net kernel's by summation order only.
+//
+// Prologue (round 6). The recurrences need W_hh and GI(0); GI(0) needs X1(0) and W_ih; X1(0) needs the gathered inputs
+// and W1. Round 5 staged W_hh and then W_ih through LDS one after the other and read W1 lane by lane (64 cache lines a
+// load instruction through L1), so the recurrences started ~58k cycles in (stamps). Now the producers load W1, W_ih
+// and W2 straight into their fragment registers at kernel entry, with K maps chosen so the four lane groups of a load
+// instruction read one contiguous 32 / 64-byte run of a weight row (16 lines an instruction), while the other four
+// waves stage W_hh through LDS (coalesced 16-byte loads, 16-byte groups XOR-swizzled by row, so the recurrence lanes'
+// pick-up reads are conflict-free at pitch 64). Three barriers: S1 (W_hh staged, xin(0)), S2 (X1(0), xin(1), W_hh
+// picked up), S3 (GI(0), X1(1), xin(2)); then the T loop.
 #pragma once
 #include "gru_fwd_fused.hpp"
 
 namespace mq {
 
-constexpr int PSP = H + 4;   // pitch of a W_hh / W_ih row staged in LDS during the prologue
-
 struct alignas(16) PairLds {
   float h0[H];                    // init_hidden: zeros
+  int psync[4];                   // LDS counters: [0] the producers' chunk-0 rendezvous (X1(1), xin(2) complete),
+                                  // [1] the hypernet waves' (their staged states)
   float xin[2][FCH][FXP];         // [chunk & 1] agent inputs (both nets)
-  // from here on, the prologue's weight staging area ([net][192 rows][PSP]) overlays the T loop's buffers
+  float x1[2][2][FCH][H + 4];     // [net][chunk & 1] X1 (written by fc1(0) while W_hh is still staged)
+  // from here on, the prologue's W_hh staging area ([net][192 rows][64], XOR-swizzled) overlays the T loop's buffers
   float hs[2][2][FCH][H + 4];     // [net][chunk & 1][step][unit]: h_t (the recurrence's h_{t-1}, fc2's operand)
   float gi[2][2][FCH][G3];        // [net][chunk & 1][step][gate column]
-  float x1[2][2][FCH][H + 4];     // [net][chunk & 1] X1
   f32x4 grec[2][FCH][H];          // [chunk & 1][step][unit] online gate record (r, z, n, W_hn h + b_hn)
 };
-static_assert(sizeof(PairLds) - offsetof(PairLds, hs) >= 2 * G3 * PSP * sizeof(float), "weight staging fits");
+static_assert(sizeof(PairLds) - offsetof(PairLds, hs) >= 2 * G3 * H * sizeof(float), "W_hh staging fits");
+constexpr int kPairPrologueBarriers = 3;   // S1, S2, S3
 
 inline bool pair_fwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_fwd_ok(I, O, A, n, RT); }
 
-// STAMP (diagnostic, MQ_DIAG pair_stamp=<file>; Tp <= 512): s_memtime stamps of the first 8 workgroups (cdna_hip_programming.md
-// §7 form: s_memtime + lgkmcnt(0) in one asm statement), kept in LDS and written to w.slab_rnn as uint32
-// [block][16 + 2 * 512] at the end: [0] kernel entry, [1] recurrence loop start, [2] its end, [3] producers'
-// prologue done, [4] the hypernet epilogue's end, producers' [5] loads issued, [6] loads landed, [7] X1(0..1) done,
-// [8] GI(0) done, [9] recurrence's W_hh landed, [11 .. 14] the hypernet waves' S3 .. chunk-0 intervals, [15] their
-// exit; producer 0's prologue: [16] after S1, [17] its gather and W1 loads issued, [18] after S2, [19] xin(0) stored,
-// [20] after S3, [21] after S4, [22] after S5; [32 + t] the recurrence's step t end; [32 + 512 + t] the producers'
-// arrival at the barrier closing the chunk of step t (chunk ends only).
+// STAMP (diagnostic, MQ_DIAG pair_stamp=<file>; Tp <= 512): s_memtime stamps of the first 8 workgroups
+// (cdna_hip_programming.md §7 form: s_memtime + lgkmcnt(0) in one asm statement), kept in LDS and written to
+// w.slab_rnn as uint32 [block][PSH + 2 * 512] at the end: [0] kernel entry, [1] recurrence loop start, [2] its end,
+// [4] the kernel's end, W_hh staging: wave 0's first loads issued [10], all stored [5]; the hypernet waves' states
+// staged [3]; [8] producer 0 at S3 (GI(0), X1(1), xin(2) done), [9] the recurrence's W_hh picked up,
+// [11 .. 13] the hypernet waves' S1 / S2 / chunk-0 intervals done, [15] their exit; producer 0: [16] its entry loads
+// issued, [17] xin(0) stored, [18] after S1, [19] X1(0) and xin(1) done, [20] after S2; [PSH + t] the recurrence's
+// step t end; [PSH + 512 + t] the producers' arrival at the barrier closing the chunk of step t (chunk ends only).
 constexpr int PSH = 32;   // header slots
 constexpr int PST = PSH + 2 * 512;
 MQ_DEV uint32_t stamp_now() {
@@ -59,31 +70,29 @@ MQ_DEV uint32_t stamp_now() {
   return (uint32_t)t;
 }
 // ---- HYP = 2: the QMIX hypernet (qmix.py:30-44) for block hb = r (32 state rows of net hb & 1) on waves 4 and 5,
-// which otherwise only pass barriers. Those waves share SIMDs s0 / s1 with the recurrences, whose matrix cores are
-// idle; in the prologue the recurrences themselves wait for the producers' first chunks (~25k cycles, stamps), so the
-// hypernet's MFMAs mostly fill dead time there, and the rest is spread thinly over the T loop's chunks. Wave hw owns
+// which otherwise only stage W_hh and pass barriers. Those waves share SIMDs s0 / s1 with the recurrences, whose
+// matrix cores are idle; in the prologue the recurrences themselves wait for the producers' first chunk, so the
+// hypernet's MFMAs fill dead time there, and the rest is spread thinly over the T loop's chunks. Wave hw owns
 // N-tiles hw, hw + 2, .. of NH / 16, both 16-row M-tiles each; the A operand (states, zero K padding) is staged once
 // in LDS, the B fragments come straight from the parameters (one tile ahead, in registers). Operand maps, K order and
 // bias add are hyper_ws_kernel's: HYP and S0 are bitwise its outputs.
 constexpr int HT_SP = 4 * 48 + 4;   // row pitch of the staged states (K padded to 192, zeros)
-// Tiles a wave has finished by the end of the interval that barrier i (0 = S1) opens, from the schedule `hs`: nibbles
-// 0..3 the cumulative counts after the S3, S4, S5 and chunk-0 intervals (the prologue's slack: the recurrences wait
-// for the producers' first chunks there), nibble 4 the tiles left for the interval after the last chunk barrier
-// (beside the producers' last fc2 and records); the rest spread evenly over chunks 1 .. cl, where every MFMA delays
-// the recurrence wave sharing the SIMD by about its own issue time (stamps, round 5).
+// Tiles a wave has finished by the end of the interval that barrier i (0 = S1, 1 = S2, 2 = S3, which opens chunk 0;
+// 3 + c closes chunk c) opens, from the schedule `hs`: nibbles 0..2 the cumulative counts after the S1, S2 and
+// chunk-0 intervals, nibble 4 the tiles left for the interval after the last chunk barrier (beside the producers'
+// last fc2 and records); the rest spread evenly over chunks 1 .. cl, where every MFMA delays the recurrence wave
+// sharing the SIMD by about its own issue time (stamps, round 5).
 MQ_DEV int hyp_tiles_by(int i, int cnt, int nbar, int hs) {
-  if (i < 2) return 0;
-  if (i < 6) return min(cnt, (hs >> (4 * (i - 2))) & 15);
   if (i >= nbar - 1) return cnt;
-  const int c5 = min(cnt, (hs >> 12) & 15), rem = max(cnt - c5 - ((hs >> 16) & 15), 0);
-  const int nl = nbar - 7;   // chunks 1 .. cl (i = 6 .. nbar - 2)
-  return min(cnt, c5 + (rem * (i - 5) + nl - 1) / nl);
+  if (i < 3) return min(cnt, (hs >> (4 * i)) & 15);
+  const int c2 = min(cnt, (hs >> 8) & 15), rem = max(cnt - c2 - ((hs >> 16) & 15), 0);
+  const int nl = nbar - 4;   // chunks 1 .. cl (i = 3 .. nbar - 2)
+  return min(cnt, c2 + (rem * (i - 2) + nl - 1) / nl);
 }
-constexpr int kHypSched = 0x08642;
-template <bool STAMP, class StageWih>
+constexpr int kHypSched = 0x10421;
+template <bool STAMP>
 MQ_DEV void hyper_waves(const Dims& d, const Rep& rp, const float* __restrict__ P0, const float* __restrict__ P1,
-                        const Lay& L, const Work& w, float* hst, uint32_t* stl, int nbar, int hsched,
-                        StageWih stage_wih) {
+                        const Lay& L, const Work& w, float* hst, uint32_t* stl, int nbar, int hsched, int* hsync) {
   const int lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
   const int hw = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) - 4;
   const int hb = blockIdx.x, S = d.S, NH = d.NH, E = d.E, nE = d.n * d.E;
@@ -91,9 +100,11 @@ MQ_DEV void hyper_waves(const Dims& d, const Rep& rp, const float* __restrict__ 
   const int z = hb & 1, m0 = (hb >> 1) * 32;
   const float* __restrict__ P = z ? P1 : P0;
   const int NT = NH / 16, cnt = act ? (NT - hw + 1) / 2 : 0;
-  // states: wave hw gathers rows 16 hw .. 16 hw + 15 (lanes: columns l, l + 64, l + 128) and stages them
+  // states: wave hw gathers rows 16 hw .. 16 hw + 15 (lanes: columns l, l + 64, l + 128) and stages them. The
+  // gather (replay rows scattered over HBM, ~10k cycles at the kernel's start) stays in flight across S1, and the two
+  // waves meet on an LDS counter after their stores, so it delays neither S1 nor any other wave.
+  float vs[16][3];
   if (act) {
-    float vs[16][3];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int m = min(m0 + 16 * hw + i, d.M - 1), t = (int)fdiv((uint32_t)m, d.dB), b = m - t * d.B;
@@ -101,6 +112,9 @@ MQ_DEV void hyper_waves(const Dims& d, const Rep& rp, const float* __restrict__ 
 #pragma unroll
       for (int cg = 0; cg < 3; ++cg) vs[i][cg] = row[min(lane + 64 * cg, S - 1)];
     }
+  }
+  lds_barrier();   // S1
+  if (act) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int ii = 16 * hw + i, m = m0 + ii;
@@ -113,8 +127,10 @@ MQ_DEV void hyper_waves(const Dims& d, const Rep& rp, const float* __restrict__ 
       }
     }
   }
-  lds_barrier();   // S2: states staged (read after S3)
-  stage_wih();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's state rows are in LDS
+  if (lane == 0) __hip_atomic_fetch_add(hsync, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (__hip_atomic_load(hsync, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 2) __builtin_amdgcn_s_sleep(1);
+  if constexpr (STAMP) { const uint32_t v = stamp_now(); if (hw == 0 && lane == 0) stl[3] = v; }
   const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)P, (short)0, (int)(L.o[MQ_P_COUNT] * sizeof(float)), 0x00020000);
   const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
@@ -154,12 +170,13 @@ MQ_DEV void hyper_waves(const Dims& d, const Rep& rp, const float* __restrict__ 
   };
   if (cnt > 0) fetch(0, ba, bja);
   int done = 0;
-  for (int i = 2; i < nbar; ++i) {
-    lds_barrier();   // barrier i (S3 .. the last chunk's)
-    // tiles go in pairs (even k on set a, odd on set b) so both register sets keep fixed roles, and every prefetch
-    // is unconditional (past the last tile a harmless repeat): with a set chosen at run time, or a prefetch behind a
-    // branch, the compiler joined the sets with copies and waited for the loads just issued (ISA, round 5)
-    const int upto = i < nbar - 1 ? hyp_tiles_by(i, cnt, nbar, hsched) & ~1 : cnt;
+  for (int i = 0; i < nbar; ++i) {
+    if (i > 0) lds_barrier();   // barrier i (S1 was passed above, .. the last chunk's)
+    // tiles go in pairs (set a holds the next tile at the top of the loop, set b its successor) so both register
+    // sets keep fixed roles, and every prefetch is unconditional (past the last tile a harmless repeat): with a set
+    // chosen at run time, or a prefetch behind a branch, the compiler joined the sets with copies and waited for the
+    // loads just issued (ISA, round 5); an odd count refills set a itself after its tile
+    const int upto = hyp_tiles_by(i, cnt, nbar, hsched);
     while (done + 1 < upto) {   // wave-uniform
       fetch(min(done + 1, cnt - 1), bb, bjb);
       tile(done, ba, bja);
@@ -167,12 +184,13 @@ MQ_DEV void hyper_waves(const Dims& d, const Rep& rp, const float* __restrict__ 
       tile(done + 1, bb, bjb);
       done += 2;
     }
-    if (done < upto) {   // the odd last tile (final interval only)
+    if (done < upto) {   // an odd tile: set a is free again once its MFMAs have read it
       tile(done, ba, bja);
+      fetch(min(done + 1, cnt - 1), ba, bja);
       ++done;
     }
     if constexpr (STAMP) {
-      if (hw == 0 && i >= 2 && i < 6) { const uint32_t v = stamp_now(); if (lane == 0) stl[9 + i] = v; }
+      if (hw == 0 && i < 3) { const uint32_t v = stamp_now(); if (lane == 0) stl[11 + i] = v; }
     }
   }
   if constexpr (STAMP) { const uint32_t v = stamp_now(); if (hw == 0 && lane == 0) stl[15] = v; }
@@ -196,71 +214,72 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
   };
 
   if (tid < H) S.h0[tid] = 0.0f;
-  constexpr int kPrologueBarriers = 6;
+  if (tid < 2) S.psync[tid] = 0;
   const bool producer = (wv & 2) != 0;
-  // Every workgroup needs both nets' W_hh (recurrences) and W_ih (producers) in registers in a lane layout whose direct
-  // loads hit 32-64 cache lines per instruction; through L1 that took ~15k cycles at the kernel's start (stamps,
-  // round 5). So they are read with coalesced 16-byte loads (a wave covers 1 KB per instruction), staged in LDS
-  // ([net][row][PSP], over the T loop's buffers), and picked up from there: W_hh by all waves before barrier S1, W_ih
-  // by the producer and idle waves between S2 and S3.
+  // W_hh of both nets reaches the recurrence waves' registers through LDS: lane j needs rows j, 64 + j, 128 + j whole,
+  // and loading that layout directly hits 64 cache lines per instruction (~15k cycles through L1, round 5). Waves
+  // 0, 1, 4 and 5 read it with coalesced 16-byte loads (a wave covers 1 KB per instruction) into [net][row][64] over
+  // the T loop's buffers, the 16-byte group c4 of row q at position c4 ^ (q & 15), so the pick-up (lane j reads group
+  // k4 of its rows) touches 16 distinct 4-bank groups per 16 lanes. Each workgroup starts at a different sixteenth of
+  // the rows, so the 256 CUs do not request the same L2 lines at the same time.
   float* const stg = &S.hs[0][0][0][0];
-  // (each workgroup starts at a different sixteenth of the rows, so the 256 CUs do not request the same L2 lines at
-  // the same time)
   const int srot = (int)(blockIdx.x & 15);
-  auto stage_rows = [&](int o_param, int nthr, int t0) {   // [2 nets][192][64] floats from P0 / P1 at o_param
-    constexpr int NV = 2 * G3 * H / 4;
-    for (int e0 = 0; e0 < NV; e0 += 16 * nthr) {
-      f32x4 v[16];
-      int ev[16];
+  auto stage_whh = [&](int st) {   // st: this thread's index among the 128 staging threads (waves 0, 1)
+    constexpr int NV = 2 * G3 * H / 4, NQ = 24, NR = NV / 128 / NQ;   // two rounds of 24 loads in flight
+    const int o_param = (int)L.o[MQ_P_RNN_W_HH];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        ev[q] = e0 + t0 + nthr * ((q + srot) & 15);
-        const int e = min(ev[q], NV - 1), z = e >= NV / 2, rem = 4 * (e - z * (NV / 2));
+    for (int rnd = 0; rnd < NR; ++rnd) {
+      f32x4 v[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int e = st + 128 * ((NQ * rnd + q + srot) % (NQ * NR)), z = e >= NV / 2, rem = 4 * (e - z * (NV / 2));
         v[q] = *(const f32x4*)((z ? P1 : P0) + o_param + rem);
       }
+      if (wv == 0 && rnd == 0) stamp(10);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int e = ev[q], z = e >= NV / 2, rem = 4 * (e - z * (NV / 2));
-        if (e < NV) *(f32x4*)&stg[(z * G3 + (rem >> 6)) * PSP + (rem & 63)] = v[q];
+      for (int q = 0; q < NQ; ++q) {
+        const int e = st + 128 * ((NQ * rnd + q + srot) % (NQ * NR)), z = e >= NV / 2, rem = 4 * (e - z * (NV / 2));
+        const int row = rem >> 6, c4 = (rem >> 2) & 15;
+        *(f32x4*)&stg[((z * G3 + row) * 16 + (c4 ^ (row & 15))) * 4] = v[q];
       }
     }
+    if (wv == 0) stamp(5);
   };
-  stage_rows((int)L.o[MQ_P_RNN_W_HH], 512, tid);
-  lds_barrier();   // S1: W_hh staged
+  const int nbar = kPairPrologueBarriers + cl + 1;
 
   if (!producer) {
-    if (wv >= 2) {   // waves 4, 5 (the recurrence SIMDs' second slots)
+    if (wv >= 4) {   // waves 4, 5 (the recurrence SIMDs' second slots)
       if constexpr (HYP == 2) {
-        hyper_waves<STAMP>(d, rp, P0, P1, L, w, hst, stl, kPrologueBarriers + cl + 1, hsched,
-                           [&]() { stage_rows((int)L.o[MQ_P_RNN_W_IH], 384, 64 * (wv - 4) + lane); });
+        hyper_waves<STAMP>(d, rp, P0, P1, L, w, hst, stl, nbar, hsched, &S.psync[1]);
         return;
       }
-      lds_barrier();   // S2
-      stage_rows((int)L.o[MQ_P_RNN_W_IH], 384, 64 * (wv - 4) + lane);   // with the producers: threads 0..127 of 384
-      for (int i = 2; i < kPrologueBarriers + cl + 1; ++i) lds_barrier();
+      for (int i = 0; i < nbar; ++i) lds_barrier();
       return;
     }
     // ================================================================ recurrence wave of net z (wave z)
     const int z = wv, j = lane;
     const float* __restrict__ P = z ? P1 : P0;
+    const float bhr = P[L.o[MQ_P_RNN_B_HH] + j], bhz = P[L.o[MQ_P_RNN_B_HH] + H + j],
+                bhn = P[L.o[MQ_P_RNN_B_HH] + 2 * H + j];
+    stage_whh(wv * 64 + lane);
+    lds_barrier();   // S1: W_hh staged (xin(0) too)
     f32x2 wr[32], wz[32], wn[32];   // W_hh[gate * 64 + j][2 k, 2 k + 1], from the staged rows
     {
-      const float* Whh = stg + (z * G3 + j) * PSP;
+      const float* Whh = stg + (z * G3 + j) * 64;
 #pragma unroll
       for (int k4 = 0; k4 < 16; ++k4) {
-        const f32x4 a = *(const f32x4*)(Whh + (0 * H) * PSP + 4 * k4);
-        const f32x4 b = *(const f32x4*)(Whh + (1 * H) * PSP + 4 * k4);
-        const f32x4 c = *(const f32x4*)(Whh + (2 * H) * PSP + 4 * k4);
+        const int o = 4 * (k4 ^ (j & 15));
+        const f32x4 a = *(const f32x4*)(Whh + (0 * H) * 64 + o);
+        const f32x4 b = *(const f32x4*)(Whh + (1 * H) * 64 + o);
+        const f32x4 c = *(const f32x4*)(Whh + (2 * H) * 64 + o);
         wr[2 * k4] = f32x2{a[0], a[1]}; wr[2 * k4 + 1] = f32x2{a[2], a[3]};
         wz[2 * k4] = f32x2{b[0], b[1]}; wz[2 * k4 + 1] = f32x2{b[2], b[3]};
         wn[2 * k4] = f32x2{c[0], c[1]}; wn[2 * k4 + 1] = f32x2{c[2], c[3]};
       }
     }
-    const float bhr = P[L.o[MQ_P_RNN_B_HH] + j], bhz = P[L.o[MQ_P_RNN_B_HH] + H + j],
-                bhn = P[L.o[MQ_P_RNN_B_HH] + 2 * H + j];
-    drain_vmem();
     if (z == 0) stamp(9);
-    for (int i = 1; i < kPrologueBarriers; ++i) lds_barrier();   // S2 (W_hh copied out) .. S6
+    lds_barrier();   // S2: W_hh picked up (the staging area is free)
+    lds_barrier();   // S3: GI(0)
     const bool online = z == 0;
     float hprev = 0.0f;
     if (z == 0) stamp(1);
@@ -334,27 +353,44 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
     f_ld = *(const int*)(rp.filled + slot0 + t);
     a_ld = *(const int*)(rp.actions + (slot0 + t) * n + ag);
   };
-  if (pw == 0) stamp(16);
   issue_gather(0);
-  if (pw == 0) stamp(17);
-  // register-resident weights of both nets: W1 (fc1 B fragments of N-tile pw), W_ih (3 N-tiles), W2 (K = 64), as
-  // 16-byte loads (W_ih / W2 rows are 64 floats at offsets that are multiples of 4; W1's rows when I % 4 == 0,
-  // otherwise element by element), every load of the prologue in flight at once
+  // register-resident weights of both nets, loaded straight from the parameters with every load of the prologue in
+  // flight at once: W1 (fc1 B fragments of N-tile pw), W_ih (GI's, N-tiles 3 pw .. 3 pw + 2), W2 (fc2's, K = 64).
+  // K orders (A and B agree; both differ from gru_fwd_fused_kernel's only in summation order): fc1's slot q of lane
+  // group g is K = 8 (q / 2) + 2 g + q % 2, GI's slot 4 kq + e is K = 16 kq + 4 g + e, so the four lane groups of
+  // one load instruction read one contiguous 32- / 64-byte run of each of 16 weight rows (16 cache lines, not 64)
   float w1r[2][FKQ], wih[2][3][16], w2r[16], bih[2][3], b1[2], b2;
 #pragma unroll
   for (int z = 0; z < 2; ++z) {
     const float* __restrict__ P = z ? P1 : P0;
-    const float* W1 = P + L.o[MQ_P_FC1_W] + (int64_t)(16 * pw + c16) * I + g * Kq;
-    if ((I & 3) == 0) {
+    // (addresses clamped into the row, out-of-range slots zeroed after the load: no exec-masked load branches)
+    const float* W1 = P + L.o[MQ_P_FC1_W] + (int64_t)(16 * pw + c16) * I;
+    if ((I & 1) == 0) {   // rows 8-byte aligned; 8 jj + 2 g < I covers the pair
 #pragma unroll
-      for (int m = 0; m < FKQ / 4; ++m) {
-        const f32x4 v = 4 * m < Kq ? *(const f32x4*)(W1 + 4 * m) : f32x4{0, 0, 0, 0};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w1r[z][4 * m + e] = (g * Kq + 4 * m + e < I) ? v[e] : 0.0f;
+      for (int jj = 0; jj < FKQ / 2; ++jj) {
+        const int k = 8 * jj + 2 * g;
+        const f32x2 v = *(const f32x2*)(W1 + min(k, I - 2));
+        const bool ok = 2 * jj < Kq && k < I;
+        w1r[z][2 * jj] = ok ? v[0] : 0.0f;
+        w1r[z][2 * jj + 1] = ok ? v[1] : 0.0f;
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < FKQ; ++k) w1r[z][k] = (k < Kq && g * Kq + k < I) ? W1[min(k, I - 1 - g * Kq)] : 0.0f;
+      for (int q = 0; q < FKQ; ++q) {
+        const int k = 8 * (q >> 1) + 2 * g + (q & 1);
+        const float v = W1[min(k, I - 1)];
+        w1r[z][q] = (q < Kq && k < I) ? v : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const float* Wi = P + L.o[MQ_P_RNN_W_IH] + (int64_t)(16 * (3 * pw + s) + c16) * H + 4 * g;
+#pragma unroll
+      for (int kq = 0; kq < 4; ++kq) {
+        const f32x4 v = *(const f32x4*)(Wi + 16 * kq);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) wih[z][s][4 * kq + e] = v[e];
+      }
     }
 #pragma unroll
     for (int s = 0; s < 3; ++s) bih[z][s] = P[L.o[MQ_P_RNN_B_IH] + 16 * (3 * pw + s) + c16];
@@ -408,15 +444,13 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
   };
   auto fc1 = [&](int z, int cc) {   // X1 of chunk cc (inputs in xin[cc & 1]), N-tile pw -> x1[z][cc & 1]
     f32x4 acc = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0};
-    const float* xa = &S.xin[cc & 1][c16][g * Kq];
+    const float* xa = &S.xin[cc & 1][c16][2 * g];
 #pragma unroll
-    for (int m = 0; m < FKQ / 4; ++m) {
-      if (4 * m >= Kq) break;
-      const f32x4 av = *(const f32x4*)&xa[4 * m];
-      acc = mfma16x4(av[0], w1r[z][4 * m], acc);
-      acc2 = mfma16x4(av[1], w1r[z][4 * m + 1], acc2);
-      acc = mfma16x4(av[2], w1r[z][4 * m + 2], acc);
-      acc2 = mfma16x4(av[3], w1r[z][4 * m + 3], acc2);
+    for (int jj = 0; jj < FKQ / 2; ++jj) {
+      if (2 * jj >= Kq) break;
+      const f32x2 av = *(const f32x2*)&xa[8 * jj];
+      acc = mfma16x4(av[0], w1r[z][2 * jj], acc);
+      acc2 = mfma16x4(av[1], w1r[z][2 * jj + 1], acc2);
     }
     const int t0 = FCH * cc;
     const auto xb = buf_rsrc(X1o + ((int64_t)t0 * R + r) * H);   // wave-uniform
@@ -433,7 +467,7 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
     f32x4 accg[3] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll
     for (int kq = 0; kq < 4; ++kq) {
-      const f32x4 av = *(const f32x4*)&S.x1[z][cc & 1][c16][16 * g + 4 * kq];
+      const f32x4 av = *(const f32x4*)&S.x1[z][cc & 1][c16][16 * kq + 4 * g];
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -481,56 +515,48 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
     }
   };
 
-  // ---- prologue (barriers S2 .. S6 after S1, matched by the other waves): W_ih staged and picked up, xin(0),
-  // xin(1) -> X1(0), X1(1) -> GI(0); xin(2) staged
-  if (pw == 0) stamp(5);
-  lds_barrier();   // S2: the recurrences have copied W_hh out of the staging area
-  if (pw == 0) stamp(18);
-  stage_rows((int)L.o[MQ_P_RNN_W_IH], 384, 128 + ptid);
-  drain_vmem();
-  if (pw == 0) stamp(6);
-  store_gather(0);
+  // ---- prologue (S1 .. S3, matched by the other waves): xin(0); X1(0), xin(1); GI(0). The recurrences start once
+  // GI(0) is in LDS; X1(1) and xin(2), which only chunk 0's producer work needs, are built inside chunk 0 behind a
+  // producers-only rendezvous (an LDS counter), so they are off the loop's start.
+  if (pw == 0) stamp(16);
+  store_gather(0);   // waits for the gather only: the weight loads issued after it stay in flight
   if (cl >= 1) issue_gather(1);
+  if (pw == 0) stamp(17);
+  lds_barrier();   // S1: xin(0) (and W_hh staged for the recurrences)
+  if (pw == 0) stamp(18);
+  fc1(0, 0);
+  fc1(1, 0);
+  if (cl >= 1) { store_gather(1); if (cl >= 2) issue_gather(2); }
   if (pw == 0) stamp(19);
-  lds_barrier();   // S3: W_ih staged
+  lds_barrier();   // S2: X1(0), xin(1); the recurrences have W_hh (the staging area under gi is free)
   if (pw == 0) stamp(20);
-#pragma unroll
-  for (int z = 0; z < 2; ++z)
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const float* Wi = stg + (z * G3 + 16 * (3 * pw + s) + c16) * PSP + 16 * g;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 v = *(const f32x4*)(Wi + 4 * q);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) wih[z][s][4 * q + e] = v[e];
-      }
-    }
-  if (cl >= 1) { drain_vmem(); store_gather(1); }
-  if (cl >= 2) issue_gather(2);
-  if (pw == 0) stamp(3);
-  lds_barrier();   // S4: W_ih copied out (the staging area is free), xin(0), xin(1)
-  if (pw == 0) stamp(21);
-#pragma unroll
-  for (int z = 0; z < 2; ++z) {
-    fc1(z, 0);
-    if (cl >= 1) fc1(z, 1);
-  }
-  if (pw == 0) stamp(7);
-  lds_barrier();   // S5: X1(0), X1(1); xin(0) free
-  if (pw == 0) stamp(22);
-  if (cl >= 2) { store_gather(2); if (cl >= 3) issue_gather(3); }
-#pragma unroll
-  for (int z = 0; z < 2; ++z) gi(z, 0);
+  gi(0, 0);
+  gi(1, 0);
   if (pw == 0) stamp(8);
-  lds_barrier();   // S6: GI(0), xin(2)
+  lds_barrier();   // S3: GI(0)
 
-  for (int c = 0; c <= cl; ++c) {
+  // chunk 0 (the recurrences run steps 0 .. 15 meanwhile): X1(1) and xin(2) first, then the steady-state work
+  if (cl >= 1) {
+    fc1(0, 1);
+    fc1(1, 1);
+    if (cl >= 2) { store_gather(2); if (cl >= 3) issue_gather(3); }
+    // every producer's X1(1) N-tile and xin(2) rows are in LDS before any producer reads them: each wave's LDS
+    // writes complete before its count, and the reads follow the wait (the recurrence waves are not involved)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS stores done
+    if (lane == 0) __hip_atomic_fetch_add(&S.psync[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(&S.psync[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4)
+      __builtin_amdgcn_s_sleep(1);
+    gi(0, 1);
+    gi(1, 1);
+  }
+  if (cl >= 2) { fc1(0, 2); fc1(1, 2); }
+  if (cl >= 3) { store_gather(3); if (cl >= 4) issue_gather(4); }
+  if (pw == 0) stamp(PSH + 512 + min(FCH - 1, Tp - 1));
+  lds_barrier();
+  for (int c = 1; c <= cl; ++c) {
     // chunk c: the recurrences run steps 16 c .. 16 c + 15 meanwhile
-    if (c >= 1) {
-      if (pw < 2) fc2(c - 1);
-      store_records(c - 1);
-    }
+    if (pw < 2) fc2(c - 1);
+    store_records(c - 1);
     if (c + 1 <= cl) { gi(0, c + 1); gi(1, c + 1); }
     if (c + 2 <= cl) { fc1(0, c + 2); fc1(1, c + 2); }
     if (c + 3 <= cl) { store_gather(c + 3); if (c + 4 <= cl) issue_gather(c + 4); }

@@ -11,17 +11,17 @@ a = np.fromfile(path, dtype=np.uint32)[-8 * PST:].reshape(8, PST).astype(np.int6
 rel = (a - a[:, :1]) % (1 << 32)
 entry, lstart, lend, pro, kend = (rel[:, i] for i in range(5))
 steps = rel[:, PSH:PSH + Tp]
-print("per block (mean of 8): recurrence loop starts at %.0f, producers' prologue done at %.0f, loop ends at %.0f,"
-      " kernel ends at %.0f cycles" % (lstart.mean(), pro.mean(), lend.mean(), kend.mean()))
+print("per block (mean of 8): recurrence loop starts at %.0f, loop ends at %.0f, kernel ends at %.0f cycles" %
+      (lstart.mean(), lend.mean(), kend.mean()))
 per = np.diff(steps, axis=1)
 t = np.arange(1, Tp)
 ins = (t % 16) != 0
-print("producers: loads issued %.0f, landed %.0f, X1(0..1) %.0f, GI(0) %.0f; recurrence W_hh landed %.0f" %
-      tuple(rel[:, i].mean() for i in (5, 6, 7, 8, 9)))
-print("producer 0's prologue: S1 %.0f, gather issued %.0f, W1 / W2 issued %.0f, S2 %.0f, W_ih staged %.0f, xin(0) %.0f, "
-      "S3 %.0f, W_ih picked + xin(1) %.0f, S4 %.0f, X1(0..1) %.0f, S5 %.0f, GI(0) %.0f" %
-      tuple(rel[:, i].mean() for i in (16, 17, 5, 18, 6, 19, 20, 3, 21, 7, 22, 8)))
-print("hypernet waves (HYP=2): tiles done in the S3/S4/S5/chunk-0 intervals %s, exit %.0f" % ([round(rel[:, 11 + i].mean()) for i in range(4)], rel[:, 15].mean()))
+print("W_hh staging: wave 0 first loads issued %.0f, all stored %.0f; hypernet states staged %.0f; recurrence W_hh "
+      "picked up %.0f" % tuple(rel[:, i].mean() for i in (10, 5, 3, 9)))
+print("producer 0's prologue: entry loads issued %.0f, xin(0) %.0f, S1 %.0f, X1(0) + xin(1) %.0f, S2 %.0f, "
+      "GI(0) + X1(1) + xin(2) %.0f" % tuple(rel[:, i].mean() for i in (16, 17, 18, 19, 20, 8)))
+print("hypernet waves (HYP=2): tiles done in the S1 / S2 / chunk-0 intervals %s, exit %.0f" %
+      ([round(rel[:, 11 + i].mean()) for i in range(3)], rel[:, 15].mean()))
 print("step cycles inside a chunk: mean %.0f, median %.0f; first step of a chunk: mean %.0f; step 0 ends %.0f after "
       "the loop start" % (per[:, ins].mean(), np.median(per[:, ins]), per[:, ~ins].mean(),
                           (steps[:, 0] - lstart).mean()))

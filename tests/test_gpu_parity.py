@@ -11,7 +11,8 @@ Two kinds of check (DESIGN.md "Parity"):
   equally valid trajectories (the oracle and the reference themselves part after 12 cfg2 steps). So at every step
   the oracle is run from the GPU's own state and every decision is classified: a near-tie (top-2 margin
   <= MARGIN_EPS * max(1, |Q|), or |fc1 pre-activation| <= RELU_EPS) is exempt, and a flip (the GPU deciding a
-  near-tie the other way) is counted. The loss must hold 1e-4 against the reference for HOLD_STEPS steps, or up to
+  near-tie the other way, either from the oracle reset to the GPU's state or from a free-running shadow oracle at its
+  own state) is counted. The loss must hold 1e-4 against the reference for HOLD_STEPS steps, or up to
   a step at or after the first counted flip. The per-step errors and counts are written to $MQ_PARITY_DIR.
 * teacher-forced steps (the per-step parity proper): the GPU learner and the numpy oracle (itself pinned to the
   reference at ~1e-7) start every step from the SAME parameters / optimiser state; the GPU's double-Q argmax
@@ -140,6 +141,10 @@ def run_case(case, check_full, plan=None):
         r["ref_loss"] = float(case.z["stat_loss"][k])
         r["shadow_loss"] = st2["loss"]
         r["shadow_flips_outside_ties"] = r2["dq_flips_outside_ties"] + r2["relu_flips_outside_ties"]
+        # near-ties the GPU decided against the free-running oracle's own decision at the oracle's own state: from
+        # such a step on, the GPU (and the shadow, which took its choices) leave the trajectory the oracle and the
+        # reference share, even where the oracle reset to the GPU's state agrees with the GPU
+        r["shadow_flips"] = r2["dq_flips"] + r2["relu_flips"]
         for s_ in STATS:
             ref = float(case.z["stat_" + s_][k])
             assert np.isfinite(st[s_]), (case.name, k, s_)
@@ -169,7 +174,7 @@ def run_case(case, check_full, plan=None):
     # every decision the GPU takes differently from the oracle at its own state is a near-tie
     for r in rec:
         assert r["dq_flips_outside_ties"] == 0 and r["relu_flips_outside_ties"] == 0, (case.name, r)
-    flip_steps = [r["step"] for r in rec if r["dq_flips"] + r["relu_flips"] > 0]
+    flip_steps = [r["step"] for r in rec if r["dq_flips"] + r["relu_flips"] + r["shadow_flips"] > 0]
     first_flip = flip_steps[0] if flip_steps else case.steps
     # against the reference's recorded actions: exact on clear margins until a flip can have moved the parameters
     for r in rec[:first_flip + 1]:
