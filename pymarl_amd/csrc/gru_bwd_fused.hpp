@@ -15,7 +15,8 @@
 //      u = 13 .. 15  dW1 += dX1^T XIN        [64 x I, K = 16]              7 / 7 / 14 MFMA
 //    and chunk 0 after the chain finishes. dW_hh / dW_ih / dW1 accumulate in the MFMA C layout for the whole T
 //    loop (48 + 48 + 28 VGPRs), so the Dx1 / Dw1 GEMMs and the dGI / dX1 buffers of the unfused path disappear.
-// Writes the per-workgroup slabs [w_ih | w_hh | b_ih | b_hh | fc2.w | fc2.b] and [fc1.w | fc1.b].
+// Writes the per-workgroup slabs [w_ih | w_hh | b_ih | b_hh | fc2.w | fc2.b] (row pitch slab_len, a multiple of 4; the
+// two matrices in the accumulators' C-tile order, see the tail) and [fc1.w | fc1.b].
 //
 // MFMA maps as gru_fwd_fused.hpp (v_mfma_f32_16x16x4_f32: A[i = c][kk = g], B[kk = g][j = c], D[4g + r][c]).
 #pragma once
@@ -63,11 +64,29 @@ inline bool fused_bwd_ok(int I, int O, int A, int n, int64_t RT) { return fused_
 // geometry in w.dwh_*): dispatched after every row, they take the CUs a second wave of rows leaves idle
 // (configs[3]'s shard, R = 320 > 256 CUs) instead of running in the reduction's launch. Same tiles, same m order:
 // bitwise dwh_red1_kernel's slabs.
-template <int DWH = 0>
+// STAMP (diagnostic, MQ_DIAG bwd_stamp=<file>; Tp <= BSTN - BSTH): s_memtime stamps of the first 8 workgroups, written to
+// w.GI (unused on this path) as uint32 [block][BSTN]: [0] entry, [1] chain wave 0 past the prologue barrier, [2] its
+// loop end, [3] producer wave 4's tail (chunk 0) done, [4] the slabs written (after the last barrier), [5] the fc2 /
+// bias slabs written; producer wave 4 in the tail: [6] dW_hh of chunk 0 done, [7] its slab stores issued, [8] past the
+// tail's first barrier, [9] dW_ih done, [10] its slab issued, [11] dX1 done; [16 + u] chain wave 0's step t = Tp - 1 - u
+// done.
+constexpr int BSTH = 16, BSTN = BSTH + 152;
+template <int DWH = 0, bool STAMP = false>
 __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, const float* __restrict__ P, Lay L,
                                                             Work w, int64_t slab_len, int64_t slab1_len) {
   __shared__ BwdFusedLds S;
   extern __shared__ float dyn[];   // W2 [A][H] | dW2 partial [A][H] | db2 [A]
+  __shared__ uint32_t bst[STAMP ? BSTN : 1];
+  auto bstamp = [&](int slot) {
+    if constexpr (STAMP) {
+      uint64_t tt;
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt)::"memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if ((threadIdx.x & 63) == 0) bst[slot] = (uint32_t)tt;
+    }
+  };
+  if (threadIdx.x == 0) bstamp(0);
   if constexpr (DWH != 0) {
     static_assert(sizeof(BwdFusedLds) >= 2 * 4 * DWH_T * (DWH_T + 1) * sizeof(float), "dW_hyper tiles reuse the LDS");
     if ((int)blockIdx.x >= d.R) {
@@ -89,30 +108,29 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
   float* dw2_s = dyn + A * H;
   float* db2_s = dyn + 2 * A * H;
 
-  {
+  // the workgroup's LDS set-up (every thread, after its role's own first loads are in flight, so the kernel start
+  // pays one memory latency, not two): W2 staged and dW2 / db2 zeroed, the history rows past Tp of the top (partial)
+  // chunk and the XIN padding zeroed, W_ih staged (dX1's B operand)
+  auto stage_common = [&]() {
     constexpr int NW2 = 16 * H / 512;   // A <= 16: all W2 loads in flight before the stores
-    float v[NW2];
+    constexpr int NW = G3 * H / 512;
+    float v2[NW2], v[NW];
 #pragma unroll
-    for (int u = 0; u < NW2; ++u) v[u] = tid + 512 * u < A * H ? P[L.o[MQ_P_FC2_W] + tid + 512 * u] : 0.0f;
-#pragma unroll
-    for (int u = 0; u < NW2; ++u)
-      if (tid + 512 * u < A * H) { w2_s[tid + 512 * u] = v[u]; dw2_s[tid + 512 * u] = 0.0f; }
-  }
-  for (int i = tid; i < A; i += 512) db2_s[i] = 0.0f;
-  // zero the history rows past Tp of the top (partial) chunk and the XIN padding
-  for (int e = tid; e < 2 * FCH * BRP; e += 512) { (&S.gh[0][0][0])[e] = 0.0f; (&S.gi[0][0][0])[e] = 0.0f; }
-  for (int e = tid; e < FCH * FXP; e += 512) (&S.xin[0][0])[e] = 0.0f;
-  {
-    constexpr int NW = G3 * H / 512;   // W_ih to LDS, all loads in flight first
-    float v[NW];
+    for (int u = 0; u < NW2; ++u) v2[u] = tid + 512 * u < A * H ? P[L.o[MQ_P_FC2_W] + tid + 512 * u] : 0.0f;
 #pragma unroll
     for (int u = 0; u < NW; ++u) v[u] = P[L.o[MQ_P_RNN_W_IH] + tid + 512 * u];
+    for (int i = tid; i < A; i += 512) db2_s[i] = 0.0f;
+    for (int e = tid; e < 2 * FCH * BRP; e += 512) { (&S.gh[0][0][0])[e] = 0.0f; (&S.gi[0][0][0])[e] = 0.0f; }
+    for (int e = tid; e < FCH * FXP; e += 512) (&S.xin[0][0])[e] = 0.0f;
+#pragma unroll
+    for (int u = 0; u < NW2; ++u)
+      if (tid + 512 * u < A * H) { w2_s[tid + 512 * u] = v2[u]; dw2_s[tid + 512 * u] = 0.0f; }
 #pragma unroll
     for (int u = 0; u < NW; ++u) {
       const int e = tid + 512 * u, m = e / H;
       S.wih[m][e - m * H] = v[u];
     }
-  }
+  };
 
   const int b = (int)fdiv((uint32_t)r, d.dN), ag = r - b * d.n;
   const int64_t* arow = rp.actions + rp.ep(b) * d.t_stride * d.n + ag;   // &actions[ep(b)][0][agent]
@@ -125,23 +143,12 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     // ================================================================ chain waves
     f32x2 wT[24];   // W_hh^T slice as pairs for v_pk_fma_f32 (K12 layout, see above)
     const int c16 = lt & 15;   // lane within the 16-lane DPP row
+    const int b3 = (c16 >> 3) & 1, b2 = (c16 >> 2) & 1, u0 = 4 * (lt >> 4);
+    f32x4 xr[12];   // W_hh rows 12 c16 .. + 11, units u0 .. u0 + 3 (loaded first, picked apart after the set-up)
     {
       const float* Whh = P + L.o[MQ_P_RNN_W_HH];
-      const int b3 = (c16 >> 3) & 1, b2 = (c16 >> 2) & 1, u0 = 4 * (lt >> 4);
-      const int a0 = u0 + 2 * b3 + b2, a1 = u0 + 2 * b3 + 1 - b2;               // pair A: the units kept
-      const int v0 = u0 + 2 * (1 - b3) + b2, v1 = u0 + 2 * (1 - b3) + 1 - b2;   // pair B: the partner's
-      // units a0, a1, v0, v1 are u0 .. u0 + 3 in a lane-dependent order: one 16-byte load per row (the compiler
-      // cannot merge the four lane-permuted dword loads itself), then selects
-      auto pick = [](const f32x4& x, int i) { return i == 0 ? x[0] : i == 1 ? x[1] : i == 2 ? x[2] : x[3]; };
-      const int i0 = a0 - u0, i1 = a1 - u0, i2 = v0 - u0, i3 = v1 - u0;
-      f32x4 xr[12];
 #pragma unroll
       for (int kk = 0; kk < 12; ++kk) xr[kk] = *(const f32x4*)(Whh + (12 * c16 + kk) * H + u0);
-#pragma unroll
-      for (int kk = 0; kk < 12; ++kk) {
-        wT[2 * kk] = f32x2{pick(xr[kk], i0), pick(xr[kk], i1)};
-        wT[2 * kk + 1] = f32x2{pick(xr[kk], i2), pick(xr[kk], i3)};
-      }
     }
     // K12 mat-vec on the 12 dgh values of this lane, reduced to the lane's unit (all four lanes of its quad)
     auto k12_sum = [&](const f32x4 (&dv)[3]) {
@@ -213,13 +220,29 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       lookup_w2(nxt);   // the next step's W2[a][k] and coefficients, beside this step's LDS reads and FMAs
       coeffs(t - 1, nxt);
       carry = fmaf(dh, cur.gz, k12_sum(dv));
+      if constexpr (STAMP) { if (tid < 64 && Tp - 1 - t < BSTN - BSTH) bstamp(BSTH + Tp - 1 - t); }
     };
     In sa, sb, sc, sd;
     load(Tp - 1, sa);
     load(Tp - 2, sb);
     load(Tp - 3, sc);
+    stage_common();
+    {
+      const int a0 = u0 + 2 * b3 + b2, a1 = u0 + 2 * b3 + 1 - b2;               // pair A: the units kept
+      const int v0 = u0 + 2 * (1 - b3) + b2, v1 = u0 + 2 * (1 - b3) + 1 - b2;   // pair B: the partner's
+      // units a0, a1, v0, v1 are u0 .. u0 + 3 in a lane-dependent order: one 16-byte load per row (the compiler
+      // cannot merge the four lane-permuted dword loads itself), then selects
+      auto pick = [](const f32x4& x, int i) { return i == 0 ? x[0] : i == 1 ? x[1] : i == 2 ? x[2] : x[3]; };
+      const int i0 = a0 - u0, i1 = a1 - u0, i2 = v0 - u0, i3 = v1 - u0;
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk) {
+        wT[2 * kk] = f32x2{pick(xr[kk], i0), pick(xr[kk], i1)};
+        wT[2 * kk + 1] = f32x2{pick(xr[kk], i2), pick(xr[kk], i3)};
+      }
+    }
     drain_vmem();
     lds_barrier();
+    if (tid == 0) bstamp(1);
     lookup_w2(sa);
     coeffs(Tp - 1, sa);
     int t = Tp - 1;
@@ -232,6 +255,7 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     if (t >= 0) lstep(t, sa, sb, sd);
     if (t - 1 >= 0) lstep(t - 1, sb, sc, sa);
     if (t - 2 >= 0) lstep(t - 2, sc, sd, sb);
+    if (tid == 0) bstamp(2);
     lds_barrier();   // producer tail: chunk 0 (2 barriers)
     lds_barrier();
     if (q < 3) { slab[o_bi + q * H + k] = db_i; slab[o_bh + q * H + k] = db_h; }
@@ -357,12 +381,13 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
       h_next = S.gh[cb][p][3 * H + k];
     };
     fc2_fetch(Tp - 1);
+    issue_rows(cl);   // the X1 / XIN rows one chunk ahead (the top chunk's up front)
+    stage_common();
 
     lds_barrier();
     for (int c = cl; c >= 0; --c) {
       const int C = c + 1;
       const bool work = C <= cl;
-      if (c == cl) issue_rows(cl);   // the X1 / XIN rows one chunk ahead (the top chunk's up front)
 #pragma unroll
       for (int u = 0; u < FCH; ++u) {
         const int t = FCH * c + FCH - 1 - u;
@@ -382,28 +407,37 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
         if (u == 5 && c < cl) issue_rows(c);   // stored at u = 4 of the next chunk
       }
     }
-    // tail: chunk 0 (2 barriers, matched by the chain waves)
+    // tail: chunk 0 (2 barriers, matched by the chain waves). Each accumulator's slab is written as soon as it is
+    // final, so the slab stores (133 KB a workgroup, every workgroup at once: HBM-bound) overlap the remaining MFMAs
+    // instead of all following them. [W_ih | W_hh] go out as the accumulators sit in the registers, one 16-byte
+    // store per lane and tile (a wave writes 1 KB contiguous per instruction; element (16 mt + 4 g + e, 16 jj + c16)
+    // at ((mt * 4 + jj) * 64 + lane) * 4 + e, which the reduction maps back: optim_kernels.hpp red_dst) instead of
+    // 48 dword stores of 4 x 64-byte runs, which the CU's memory pipeline issued at ~46 cycles each (stamps).
+    auto write_rec = [&](const f32x4 (&acc)[3][4], int64_t o) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          *(f32x4*)&slab[o + (((3 * wv + i) * 4 + jj) * 64 + lane) * 4] = acc[i][jj];
+    };
     dw_rec(0, 0, 4, false);
-    drain_vmem();
-    store_rows(0);
+    if (ptid == 0) bstamp(6);
+    store_rows(0);   // (the compiler waits for these rows' loads only, not for the slab stores below)
+    write_rec(acc_hh, o_hh);
+    if (ptid == 0) bstamp(7);
     lds_barrier();
+    if (ptid == 0) bstamp(8);
     dw_rec(0, 0, 4, true);
+    if (ptid == 0) bstamp(9);
+    write_rec(acc_ih, 0);
+    if (ptid == 0) bstamp(10);
     dx1_part(0, 0, 12);
     dx1_epi();
+    if (ptid == 0) bstamp(11);
     lds_barrier();
     dw1_part(0, 4);
+    if (ptid == 0) bstamp(3);
 
-    // per-workgroup slabs in the MFMA C layout: element (16 tile + 4 g + e, 16 tile' + c16)
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = 16 * (3 * wv + i) + 4 * g + e, nn = 16 * jj + c16;
-          slab[m * H + nn] = acc_ih[i][jj][e];
-          slab[o_hh + m * H + nn] = acc_hh[i][jj][e];
-        }
     float* slab1 = w.slab_fc1 + (int64_t)blockIdx.x * slab1_len;
 #pragma unroll
     for (int nt = 0; nt < 7; ++nt)
@@ -415,11 +449,20 @@ __global__ __launch_bounds__(512) void gru_bwd_fused_kernel(Dims d, Rep rp, cons
     S.db1[g][16 * wv + c16] = db1p;
   }
   lds_barrier();
+  if (tid == 0) bstamp(4);
   for (int i = tid; i < A * H; i += 512) slab[o_w2 + i] = dw2_s[i];
   for (int i = tid; i < A; i += 512) slab[o_b2 + i] = db2_s[i];
   if (tid < H)
     w.slab_fc1[(int64_t)blockIdx.x * slab1_len + H * I + tid] =
         (S.db1[0][tid] + S.db1[1][tid]) + (S.db1[2][tid] + S.db1[3][tid]);
+  if constexpr (STAMP) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) bstamp(5);
+    __syncthreads();
+    if (blockIdx.x < 8)
+      for (int i = tid; i < BSTN; i += 512) ((uint32_t*)w.GI)[(size_t)blockIdx.x * BSTN + i] = bst[i];
+  }
 }
 
 // Host: the fused BPTT, with dW_hyper's tiles appended (DWH = 1; w.dwh_* set by the caller) or without.
@@ -429,8 +472,11 @@ inline void launch_bwd_fused_dwh(size_t dyn, hipStream_t s, const Dims& d, const
   hipLaunchKernelGGL((gru_bwd_fused_kernel<1>), grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
 }
 inline void launch_bwd_fused(dim3 grid, size_t dyn, hipStream_t s, const Dims& d, const Rep& rp, const float* P,
-                             const Lay& L, const Work& w, int64_t slab_len, int64_t slab1_len) {
-  hipLaunchKernelGGL((gru_bwd_fused_kernel<0>), grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+                             const Lay& L, const Work& w, int64_t slab_len, int64_t slab1_len, bool stamp = false) {
+  if (stamp)
+    hipLaunchKernelGGL((gru_bwd_fused_kernel<0, true>), grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
+  else
+    hipLaunchKernelGGL((gru_bwd_fused_kernel<0>), grid, dim3(512), dyn, s, d, rp, P, L, w, slab_len, slab1_len);
 }
 
 }  // namespace mq

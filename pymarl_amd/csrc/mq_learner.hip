@@ -116,6 +116,7 @@ struct mq_handle {
   int64_t off[MQ_P_COUNT + 1];
   int64_t P;
   int64_t len_rnn, len_mix;
+  int64_t pitch_rnn;   // the fused BPTT's slab pitch: len_rnn rounded up to 4 floats (16-byte slab rows)
   // bound (caller-owned)
   float *on = nullptr, *tg = nullptr, *grad = nullptr, *sq = nullptr, *stats = nullptr;
   int32_t* curmax_user = nullptr;
@@ -191,6 +192,7 @@ void compute_layout(mq_handle* h) {
   h->off[MQ_P_COUNT] = o;
   h->P = o;
   h->len_rnn = h->off[MQ_P_FC2_B] + A - h->off[MQ_P_RNN_W_IH];
+  h->pitch_rnn = (h->len_rnn + 3) & ~int64_t(3);
   h->len_mix = h->off[MQ_P_V2_W] - h->off[MQ_P_HW1_W];
 }
 
@@ -297,10 +299,12 @@ struct RedBuilder {
   float* tmp;
   explicit RedBuilder(float* t) : tmp(t) {}
   // returns true when the region is summed by pass 2 straight from its slabs (no pass-1 blocks read them)
-  bool add(const float* src, int nslab, int64_t len, float* dst, bool sq, int64_t pitch = 0, bool direct_ok = false) {
+  bool add(const float* src, int nslab, int64_t len, float* dst, bool sq, int64_t pitch = 0, bool direct_ok = false,
+           int perm = 0) {
     if (len <= 0 || nslab <= 0) return false;
     RedRegion& R = pl.r[pl.nr++];
     R.src = src; R.dst = dst; R.len = len; R.pitch = pitch > 0 ? pitch : len; R.nslab = nslab; R.sq = sq ? 1 : 0;
+    R.perm = perm;
     if (direct_ok && nslab <= kRedZ) {   // pass 2 sums the slabs themselves: no pass-1 blocks, no tmp
       R.zc = 1; R.ng = nslab; R.tmp = (float*)src; R.tpitch = R.pitch; R.vec = 0; R.xcd = 0;
       R.blk1 = b1;
@@ -399,7 +403,7 @@ int mq_create(const mq_config* cfg, mq_handle** out) {
       RT * 3 * Hd,                                   // dGI
       RT * Hd,                                       // dP1
       nfc1 * (Hd * h->I + Hd),                       // slab_fc1
-      Rm * h->len_rnn,                               // slab_rnn (RW = 1 worst case)
+      Rm * h->pitch_rnn,                             // slab_rnn (RW = 1 worst case)
       (int64_t)kNsplitMax * h->len_mix,              // slab_mix
       nmix * (h->E + 1),                             // slab_v2
       nmix * 8,                                      // loss_part
@@ -659,10 +663,21 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     }
     const float* P0 = (const float*)h->on;
     const int64_t l1 = (int64_t)mq::H * d.I + mq::H;
+    // diagnostic (MQ_DIAG bwd_stamp=<file>): step stamps of the first 8 workgroups
+    std::string bstamp_path;
+    const bool bstamp = !dwh_in_bwd && env_item("MQ_DIAG", "bwd_stamp", &bstamp_path) && !bstamp_path.empty() &&
+                        d.Tp <= BSTN - BSTH;
     if (dwh_in_bwd) MQ_LDS(gru_bwd_fused_kernel<1>, dyn);
+    else if (bstamp) MQ_LDS((gru_bwd_fused_kernel<0, true>), dyn);
     else MQ_LDS(gru_bwd_fused_kernel<0>, dyn);
-    if (dwh_in_bwd) launch_bwd_fused_dwh(dyn, s, d, rp, P0, L, w, h->len_rnn, l1);
-    else launch_bwd_fused(dim3(d.R), dyn, s, d, rp, P0, L, w, h->len_rnn, l1);
+    if (dwh_in_bwd) launch_bwd_fused_dwh(dyn, s, d, rp, P0, L, w, h->pitch_rnn, l1);
+    else launch_bwd_fused(dim3(d.R), dyn, s, d, rp, P0, L, w, h->pitch_rnn, l1, bstamp);
+    if (bstamp) {
+      std::vector<uint32_t> st((size_t)8 * BSTN);
+      MQ_HIP(hipMemcpyAsync(st.data(), w.GI, st.size() * 4, hipMemcpyDeviceToHost, s));
+      MQ_HIP(hipStreamSynchronize(s));
+      if (FILE* f = fopen(bstamp_path.c_str(), "ab")) { fwrite(st.data(), 4, st.size(), f); fclose(f); }
+    }
     MQ_HIP(hipGetLastError());
   } else {
     {
@@ -708,7 +723,13 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     }
     RedBuilder rb(w.red_tmp);
     rb.add(w.slab_fc1, h->nsplit_fc1, (int64_t)mq::H * d.I + mq::H, h->grad + h->off[MQ_P_FC1_W], true);
-    rb.add(w.slab_rnn, h->nblk_bwd, h->len_rnn, h->grad + h->off[MQ_P_RNN_W_IH], true);
+    if (fused_bwd) {   // [W_ih | W_hh] in the BPTT's C-tile order (red_dst), then the biases and fc2
+      const int64_t lm = 2LL * mq::G3 * mq::H;
+      rb.add(w.slab_rnn, h->nblk_bwd, lm, h->grad + h->off[MQ_P_RNN_W_IH], true, h->pitch_rnn, false, 1);
+      rb.add(w.slab_rnn + lm, h->nblk_bwd, h->len_rnn - lm, h->grad + h->off[MQ_P_RNN_W_IH] + lm, true, h->pitch_rnn);
+    } else {
+      rb.add(w.slab_rnn, h->nblk_bwd, h->len_rnn, h->grad + h->off[MQ_P_RNN_W_IH], true);
+    }
     if (c.mixer == MQ_MIXER_QMIX) {
       // dW_hyper's few m-slice slabs go straight to pass 2 (they are written in the same launch as pass 1)
       const bool direct = rb.add(w.slab_mix, h->nsplit_mix, h->len_mix, h->grad + h->off[MQ_P_HW1_W], true, 0, true);

@@ -29,6 +29,7 @@ struct RedRegion {
                     // r == g (mod 8), summed by blocks with blockIdx == g (mod 8), i.e. on the XCD whose L2 holds
                     // them when slab r was written by workgroup r (the per-row BPTT slabs)
   int blk1, blk2;   // first block of this region in pass 1 / pass 2
+  int perm;         // 1: the slabs hold [W_ih | W_hh] ([2][G3][H]) in the fused BPTT's MFMA C-tile order (red_dst)
 };
 struct RedPlan {
   RedRegion r[kRedMaxRegions];
@@ -86,6 +87,16 @@ MQ_DEV void red_pass1_body(const RedPlan& pl, int blk) {
 
 __global__ __launch_bounds__(256) void red_pass1_kernel(RedPlan pl) { red_pass1_body(pl, blockIdx.x); }
 
+// Destination of region element i. perm = 1 (the fused BPTT's [W_ih | W_hh] slabs, gru_bwd_fused.hpp): the slab stores
+// each wave's accumulators as they sit in its registers, one 16-byte store per lane and tile, so element
+// p = ((mt * 4 + jj) * 64 + lane) * 4 + e of matrix z holds W[16 mt + 4 (lane >> 4) + e][16 jj + (lane & 15)].
+MQ_DEV int64_t red_dst(const RedRegion& R, int64_t i) {
+  if (!R.perm) return i;
+  const int z = (int)(i / (G3 * H)), p = (int)(i - (int64_t)z * (G3 * H));
+  const int e = p & 3, lane = (p >> 2) & 63, rest = p >> 8, jj = rest & 3, mt = rest >> 2;
+  return (int64_t)z * (G3 * H) + (16 * mt + 4 * (lane >> 4) + e) * H + 16 * jj + (lane & 15);
+}
+
 __global__ __launch_bounds__(256) void red_pass2_kernel(RedPlan pl, float* __restrict__ norm_part) {
   const int k = red_region(pl, blockIdx.x, true);
   const RedRegion& R = pl.r[k];
@@ -98,7 +109,7 @@ __global__ __launch_bounds__(256) void red_pass2_kernel(RedPlan pl, float* __res
     float v = 0.0f;
 #pragma unroll
     for (int g = 0; g < kRedZ; ++g) v += u[g];
-    R.dst[i] = v;
+    R.dst[red_dst(R, i)] = v;
     if (R.sq) sq = v * v;
   }
   __shared__ float red[4];

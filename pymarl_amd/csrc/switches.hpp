@@ -4,8 +4,9 @@
 //            noted: unfused_fwd, unfused_bwd, row_tiles=0|1, hyp_in_fwd=0|1, dwh_in_bwd=0|1, fwd_pair=0|1,
 //            pair_hyp_epi, mix_generic; COMA (read per train()): coma_chain=0, coma_overlap=0
 //   MQ_DIAG  diagnostics and test hooks, read per train(): pair_stamp=<file> (the row-pair forward's s_memtime
-//            stamps), hyp_sched=<hex> (its in-loop hypernet tile schedule), coma_trace (the COMA chain's phase
-//            times), coma_fault=<workgroup> (a chain workgroup that stops flagging)
+//            stamps), bwd_stamp=<file> (the fused BPTT's), hyp_sched=<hex> (the pair forward's in-loop hypernet tile
+//            schedule), coma_trace (the COMA chain's phase times), coma_fault=<workgroup> (a chain workgroup that
+//            stops flagging)
 #pragma once
 #include <cstdlib>
 #include <cstring>
