@@ -162,6 +162,7 @@ typedef struct mq_plan {
   int32_t mix;           /* MQ_MIX_* */
   int32_t tiles;         /* 1: the row-tile MFMA forward / BPTT of large batches (gru_fwd_tile / gru_bwd_tile);
                             fused_fwd / fused_bwd / rw_* are then 0 */
+  int32_t dwh;           /* QMIX dW_hyper: beside reduction pass 1 (0) or appended to the fused BPTT's grid (1) */
 } mq_plan;
 int mq_last_plan(const mq_handle* h, mq_plan* out);
 

@@ -79,7 +79,7 @@ class MCConfig(ctypes.Structure):
 
 class MQPlan(ctypes.Structure):
     _fields_ = [(k, ctypes.c_int32) for k in ("rows", "fused_fwd", "rw_fwd", "fused_bwd", "rw_bwd", "inline_ids",
-                                               "hyper", "mix", "tiles")]
+                                               "hyper", "mix", "tiles", "dwh")]
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}

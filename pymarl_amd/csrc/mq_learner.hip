@@ -627,6 +627,9 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
   }
   pt.begin(PH_GRUB);
   bool dwh_in_bwd = false;
+  int dwh_mode = 0;   // where dW_hyper runs (mq_plan.dwh)
+  // dW_hyper's m-slices (A/B at cfg2: 4 / 8 / 16 / 32 -> 238.5 / 235.1 / 236.3 / 237.4 us, round 1)
+  const int dwh_ns = std::max(1, std::min({h->dwh_split, kRedZ, (d.M + 1) / 2}));
   plan.fused_bwd = fused_bwd ? 1 : 0;
   plan.rw_bwd = fused_bwd || tiles ? 0 : rw_bwd;
   if (tiles) {
@@ -651,26 +654,33 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
     h->nblk_bwd = d.R;
     h->nsplit_fc1 = h->nblk_bwd;
     const size_t dyn = ((size_t)2 * d.A * mq::H + d.A) * sizeof(float);
-    dwh_in_bwd = c.mixer == MQ_MIXER_QMIX &&
-                 (h->dwh_in_bwd == 1 || (h->dwh_in_bwd < 0 && many));
-    if (dwh_in_bwd) {   // the reduction's dW_hyper blocks, same geometry (see dwh_fused below)
-      w.dwh_tj = (d.NH + DWH_T - 1) / DWH_T;
-      const int ts = (d.S + 1 + DWH_T - 1) / DWH_T;
-      w.dwh_ns = std::max(1, std::min({h->dwh_split, kRedZ, (d.M + 1) / 2}));
-      w.dwh_n = w.dwh_tj * ts * w.dwh_ns;
-      w.dwh_len = h->len_mix;
-      h->nsplit_mix = w.dwh_ns;
+    // dW_hyper: appended to the BPTT's grid when its rows exceed the CUs (mode 1: the second wave of rows leaves
+    // CUs idle), else beside pass 1 of the reduction (mode 0); MQ_PLAN dwh_in_bwd=0|1 forces one. (Round 6: its
+    // tiles on the BPTT's chain waves in the kernel's tail, idle while the producers reduce the last chunk, made the
+    // BPTT 14 us longer against the 8.6 us they took out of the reduction's launch: four waves per CU leave each
+    // tile's load round trips exposed. Removed.)
+    if (c.mixer == MQ_MIXER_QMIX) {
+      const int tj = (d.NH + DWH_T - 1) / DWH_T, ts = (d.S + 1 + DWH_T - 1) / DWH_T;
+      dwh_mode = h->dwh_in_bwd >= 0 ? (h->dwh_in_bwd ? 1 : 0) : many ? 1 : 0;
+      if (dwh_mode != 0) {   // the reduction's dW_hyper blocks, same geometry (see dwh_fused below)
+        w.dwh_tj = tj;
+        w.dwh_ns = dwh_ns;
+        w.dwh_n = tj * ts * dwh_ns;
+        w.dwh_len = h->len_mix;
+        h->nsplit_mix = dwh_ns;
+      }
     }
+    dwh_in_bwd = dwh_mode != 0;
+    plan.dwh = dwh_mode;
     const float* P0 = (const float*)h->on;
     const int64_t l1 = (int64_t)mq::H * d.I + mq::H;
     // diagnostic (MQ_DIAG bwd_stamp=<file>): step stamps of the first 8 workgroups
     std::string bstamp_path;
-    const bool bstamp = !dwh_in_bwd && env_item("MQ_DIAG", "bwd_stamp", &bstamp_path) && !bstamp_path.empty() &&
+    const bool bstamp = dwh_mode != 1 && env_item("MQ_DIAG", "bwd_stamp", &bstamp_path) && !bstamp_path.empty() &&
                         d.Tp <= BSTN - BSTH;
-    if (dwh_in_bwd) MQ_LDS(gru_bwd_fused_kernel<1>, dyn);
-    else if (bstamp) MQ_LDS((gru_bwd_fused_kernel<0, true>), dyn);
-    else MQ_LDS(gru_bwd_fused_kernel<0>, dyn);
-    if (dwh_in_bwd) launch_bwd_fused_dwh(dyn, s, d, rp, P0, L, w, h->pitch_rnn, l1);
+    if (dwh_mode == 1) MQ_LDS(gru_bwd_fused_kernel<1>, dyn);
+    else MQ_LDS((gru_bwd_fused_kernel<0, true>), dyn);   // the larger of the two builds
+    if (dwh_mode == 1) launch_bwd_fused_dwh(dyn, s, d, rp, P0, L, w, h->pitch_rnn, l1);
     else launch_bwd_fused(dim3(d.R), dyn, s, d, rp, P0, L, w, h->pitch_rnn, l1, bstamp);
     if (bstamp) {
       std::vector<uint32_t> st((size_t)8 * BSTN);
@@ -717,7 +727,7 @@ static int fb_impl(mq_handle* h, const mq_replay* batch, hipStream_t s) {
       tj = (d.NH + DWH_T - 1) / DWH_T;
       ts = (d.S + 1 + DWH_T - 1) / DWH_T;
       // pass 1 shares this launch with dW_hyper, so dW_hyper's slabs must go straight to pass 2: at most kRedZ
-      ns = std::max(1, std::min({h->dwh_split, kRedZ, (d.M + 1) / 2}));
+      ns = dwh_ns;
       h->nsplit_mix = ns;
       ndwh = tj * ts * ns;
     }

@@ -354,12 +354,13 @@ class QLearner:
 
     def last_plan(self):
         """Kernel variants the last train() launched (mq_last_plan): rows, fused_fwd, rw_fwd, fused_bwd, rw_bwd,
-        inline_ids, hyper, mix."""
+        inline_ids, hyper, mix, tiles, dwh (where QMIX's dW_hyper ran: "red1" or "bptt_grid")."""
         pl = _lib.MQPlan()
         _lib.check(self._handle.lib.mq_last_plan(self._handle.h, ctypes.byref(pl)))
         d = pl.as_dict()
         d["hyper"] = _lib.HYP_NAMES[d["hyper"]]
         d["mix"] = _lib.MIX_NAMES[d["mix"]]
+        d["dwh"] = ("red1", "bptt_grid")[d["dwh"]]
         return d
 
     def last_cur_max_actions(self):

@@ -40,7 +40,8 @@ int main(void) {
   printf("%d %d\\n", MQ_P_COUNT, MQ_NSUMS);
   printf("%zu %zu %zu %d %d %d\\n", sizeof(mc_config), offsetof(mc_config, gamma), offsetof(mc_config, max_seq),
          MC_P_COUNT, MC_NTAIL, MC_NSTATS);
-  printf("%zu %zu %zu\\n", sizeof(mq_plan), offsetof(mq_plan, inline_ids), offsetof(mq_plan, mix));
+  printf("%zu %zu %zu %zu\\n", sizeof(mq_plan), offsetof(mq_plan, inline_ids), offsetof(mq_plan, mix),
+         offsetof(mq_plan, dwh));
   return 0;
 }
 """)
@@ -53,7 +54,7 @@ int main(void) {
           ctypes.sizeof(_lib.MQReplay), _lib.MQReplay.batch_size.offset, _lib.P_COUNT, _lib.NSUMS,
           ctypes.sizeof(_lib.MCConfig), _lib.MCConfig.gamma.offset, _lib.MCConfig.max_seq.offset, _lib.MC_P_COUNT,
           _lib.MC_NTAIL, _lib.MC_NSTATS, ctypes.sizeof(_lib.MQPlan), _lib.MQPlan.inline_ids.offset,
-          _lib.MQPlan.mix.offset]
+          _lib.MQPlan.mix.offset, _lib.MQPlan.dwh.offset]
     assert c == py
 
 

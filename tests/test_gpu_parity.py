@@ -612,8 +612,8 @@ def test_avail_bits_bitwise(cases, name, generic, monkeypatch):
 @pytest.mark.parametrize("name", ["cfg2_qmix", "cfg4_qmix", "cfg1_qmix", "tiny_qmix_full"])
 def test_dwh_in_bptt_grid_bitwise(cases, name, monkeypatch):
     """dW_hyper's tiles appended to the fused BPTT's grid (MQ_PLAN dwh_in_bwd=1; the default for shards past the CU
-    count, e.g. cfg4) equal dW_hyper in the reduction's launch (MQ_PLAN dwh_in_bwd=0) bitwise: parameters, gradients,
-    square_avg and stats over up to four steps."""
+    count, e.g. cfg4) equal dW_hyper in the reduction's launch (MQ_PLAN dwh_in_bwd=0) bitwise: parameters,
+    gradients, square_avg and stats over up to four steps; the plan reports where it ran."""
     from tests.gpu_helpers import build, flat_grads, flat_params
     case = get_case(cases, name)
     outs = []
@@ -625,7 +625,8 @@ def test_dwh_in_bptt_grid_bitwise(cases, name, monkeypatch):
             batch = buf.sample(case.B)
             learner.train(batch[:, :batch.max_t_filled()], 1000 * k, case.episodes[k])
         th.cuda.synchronize()
-        assert learner.last_plan()["fused_bwd"] == 1
+        plan = learner.last_plan()
+        assert plan["fused_bwd"] == 1 and plan["dwh"] == ("bptt_grid" if inb == "1" else "red1"), plan
         outs.append((flat_params(learner), flat_grads(learner), learner._sq.cpu().numpy(), learner.last_stats()))
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.array_equal(outs[0][1], outs[1][1])
