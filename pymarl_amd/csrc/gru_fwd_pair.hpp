@@ -103,6 +103,7 @@ MQ_DEV void hyper_waves(const Dims& d, const Rep& rp, const float* __restrict__ 
   // states: wave hw gathers rows 16 hw .. 16 hw + 15 (lanes: columns l, l + 64, l + 128) and stages them. The
   // gather (replay rows scattered over HBM, ~10k cycles at the kernel's start) stays in flight across S1, and the two
   // waves meet on an LDS counter after their stores, so it delays neither S1 nor any other wave.
+  if constexpr (STAMP) { const uint32_t v = stamp_now(); if (hw == 0 && lane == 0) stl[25] = v; }
   float vs[16][3];
   if (act) {
 #pragma unroll
@@ -113,6 +114,7 @@ MQ_DEV void hyper_waves(const Dims& d, const Rep& rp, const float* __restrict__ 
       for (int cg = 0; cg < 3; ++cg) vs[i][cg] = row[min(lane + 64 * cg, S - 1)];
     }
   }
+  if constexpr (STAMP) { const uint32_t v = stamp_now(); if (hw == 0 && lane == 0) stl[26] = v; }
   lds_barrier();   // S1
   if (act) {
 #pragma unroll
@@ -259,6 +261,7 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
     // ================================================================ recurrence wave of net z (wave z)
     const int z = wv, j = lane;
     const float* __restrict__ P = z ? P1 : P0;
+    if (z == 0) stamp(24);
     const float bhr = P[L.o[MQ_P_RNN_B_HH] + j], bhz = P[L.o[MQ_P_RNN_B_HH] + H + j],
                 bhn = P[L.o[MQ_P_RNN_B_HH] + 2 * H + j];
     stage_whh(wv * 64 + lane);
@@ -353,7 +356,9 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
     f_ld = *(const int*)(rp.filled + slot0 + t);
     a_ld = *(const int*)(rp.actions + (slot0 + t) * n + ag);
   };
+  if (pw == 0) stamp(21);
   issue_gather(0);
+  if (pw == 0) stamp(22);
   // register-resident weights of both nets, loaded straight from the parameters with every load of the prologue in
   // flight at once: W1 (fc1 B fragments of N-tile pw), W_ih (GI's, N-tiles 3 pw .. 3 pw + 2), W2 (fc2's, K = 64).
   // K orders (A and B agree; both differ from gru_fwd_fused_kernel's only in summation order): fc1's slot q of lane
@@ -392,6 +397,7 @@ MQ_DEV void pair_body(const Dims& d, const Rep& rp, const float* __restrict__ P0
         for (int e = 0; e < 4; ++e) wih[z][s][4 * kq + e] = v[e];
       }
     }
+    if (pw == 0 && z == 0) stamp(23);
 #pragma unroll
     for (int s = 0; s < 3; ++s) bih[z][s] = P[L.o[MQ_P_RNN_B_IH] + 16 * (3 * pw + s) + c16];
     b1[z] = P[L.o[MQ_P_FC1_B] + 16 * pw + c16];

@@ -137,7 +137,7 @@ struct mq_handle {
   // (R = 320; round 3)
   static constexpr int fused_bwd_rmax = 512;
   // m-slices of the dW_hyper pass (A/B at cfg2, DESIGN §3: 4 / 8 / 16 / 32 -> 238.5 / 235.1 / 236.3 / 237.4 us)
-  static constexpr int dwh_split = 8;
+  int dwh_split = plan_int("dwh_split", 8);
   // the row-tile MFMA forward / BPTT (gru_tiles.hpp) for batches past the one-row fused kernels (R > 512 rows);
   // row_tiles=1 forces it on any batch it can take (tests), =0 turns it off (A/B: the unfused GEMM path)
   int row_tiles = plan_int("row_tiles", -1);

@@ -20,6 +20,8 @@ print("W_hh staging: wave 0 first loads issued %.0f, all stored %.0f; hypernet s
       "picked up %.0f" % tuple(rel[:, i].mean() for i in (10, 5, 3, 9)))
 print("producer 0's prologue: entry loads issued %.0f, xin(0) %.0f, S1 %.0f, X1(0) + xin(1) %.0f, S2 %.0f, "
       "GI(0) + X1(1) + xin(2) %.0f" % tuple(rel[:, i].mean() for i in (16, 17, 18, 19, 20, 8)))
+print("role entries: producer 0 %.0f (gather issued %.0f, net-0 W1 / W_ih issued %.0f), recurrence 0 %.0f, hypernet 0 "
+      "%.0f (state loads issued %.0f)" % tuple(rel[:, i].mean() for i in (21, 22, 23, 24, 25, 26)))
 print("hypernet waves (HYP=2): tiles done in the S1 / S2 / chunk-0 intervals %s, exit %.0f" %
       ([round(rel[:, 11 + i].mean()) for i in range(3)], rel[:, 15].mean()))
 print("step cycles inside a chunk: mean %.0f, median %.0f; first step of a chunk: mean %.0f; step 0 ends %.0f after "
