@@ -5,15 +5,16 @@
 // tile [16 units ut][CC_KW columns ks] for the whole train: the tile stays in LDS and its RMSprop square_avg and
 // gradient in registers, so W1 (the critic's 111k-element bulk at MMM2) never leaves the CU between steps. The first
 // NHEAD = ceil(R / 16) workgroups also run the head of one 16-row tile. fc1.bias / fc2 / fc3 live in P (the caller's
-// buffer): every workgroup applies the update to a 1/G slice of them in place, and the heads reload the new version
-// into LDS at the start of the next step. One live step t is four phases:
+// buffer): the lane that computes an element's gradient in phase C applies its update in place in phase D, and the
+// heads reload the new version into LDS at the start of the next step. One live step t is four phases:
 //   A  (all)   H1p[ks][r][16 ut ..] = X_t[r][K slice] W1_tile^T                         (MFMA; X_t prefetched)
 //   B  (heads) reload b1 / W2 / b2 / W3 / b3, H1 = relu(sum_ks H1p + b1), H2 = relu(H1 W2^T + b2), Q = H2 W3^T + b3,
 //              TD error vs the TD(lambda) target, loss sums, dQ, dH2 = dQ W3 o [H2 > 0], dH1 = dH2 W2 o [H1 > 0]
 //   C  (all)   dW1 tile = dH1[:, units]^T X_t[:, K slice] (registers), db1 (ks = 0), the 64 dW2 16x16 tiles and
 //              the dW3 tiles round-robin over the workgroups, per-workgroup sum of squares
 //   D  (all)   the global gradient norm from the G partials (fixed order), clip coefficient, RMSprop on the owned
-//              W1 tile and on the owned slice of fc1.bias .. fc3.bias; the last workgroup records the stats
+//              W1 tile and on the fc1.bias .. fc3.bias elements whose gradients the workgroup computed in C (still in
+//              registers: no gradient exchange); the last workgroup records the stats
 // The hand-offs are flags, not grid barriers: A -> B every workgroup flags, only the heads wait; B -> C the heads
 // flag, every workgroup waits; C -> D each workgroup publishes its sum of squares as one 8-B {value, step tag}
 // granule after draining its stores, and every workgroup's wave 0 polls all G granules. Buffers reused by the next
@@ -39,7 +40,7 @@ constexpr int CC_THREADS = 512;   // 8 waves: 2 per SIMD, so a wave may hold 256
 constexpr int CC_KW = 112;      // W1 columns per owner workgroup: 7 MFMA N-tiles, 28 k-steps
 constexpr int CC_KP = CC_KW + 1;
 constexpr int CC_MAXR = 80;     // rows (B * n) of one critic step the LDS budget allows
-constexpr int CC_CP = CH + 1;
+constexpr int CC_CP = CH + 4;   // head-array row pitch: 16-B rows for the b128 operand reads of phase B
 constexpr unsigned CC_SPIN_LIMIT = 1u << 20;
 constexpr int CC_XV = CC_KW / 4;                                     // 16-B units per X row slice
 constexpr int CC_XPT = (CC_MAXR * CC_XV + CC_THREADS - 1) / CC_THREADS;  // of them per thread
@@ -70,6 +71,7 @@ MQ_DEV f32x4 ld_wt4(const float* p) {
 }
 // 16-B write-through store (global_store_dwordx4 sc1); drained by cc_post's vmcnt(0) like every store
 MQ_DEV void st_wt4(float* p, f32x4 v) { asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(v) : "memory"); }
+constexpr int kCpolSc1 = 16;   // buffer-instruction cache policy: sc1 (write-through store / L2-coherent load)
 MQ_DEV void cc_vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 MQ_DEV void cc_ready(f32x4& v) { asm volatile("" : "+v"(v)); }
 
@@ -121,9 +123,9 @@ struct CCLds {
     h1 = b3 + A16;                    // [16][CC_CP]
     h2 = h1 + 16 * CC_CP;             // [16][CC_CP]
     dh2 = h2 + 16 * CC_CP;            // [16][CC_CP]
-    q = dh2 + 16 * CC_CP;             // [16][A16 + 1]
-    misc = q + 16 * (A16 + 1);        // 64 floats of scalars / partials
-    total = misc + 64;
+    q = dh2 + 16 * CC_CP;             // (unused: Q is consumed where it is summed)
+    misc = q;                         // 176 floats of scalars / partials (CC_MISC)
+    total = misc + 176;
   }
 };
 
@@ -197,7 +199,6 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
   float* H1s = lds + Lo.h1;
   float* H2s = lds + Lo.h2;
   float* dH2s = lds + Lo.dh2;
-  float* Qs = lds + Lo.q;
   float* misc = lds + Lo.misc;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
   const int wg = blockIdx.x, ut = wg & 7, ks = wg >> 3;
@@ -226,8 +227,33 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
     for (int e = A * CH + tid; e < A16 * CH; e += CC_THREADS) W3s[(e >> 7) * CC_CP + (e & 127)] = 0.0f;
     if (tid >= A && tid < A16) b3s[tid] = 0.0f;
   }
-  // this workgroup's slice of fc1.bias .. fc3.bias: it applies the RMSprop update of those elements every step
-  const int hper = (npart + a.NG - 1) / a.NG, h_beg = min(npart, wg * hper), h_end = min(npart, h_beg + hper);
+  // fc1.bias .. fc3.bias: every element's gradient is computed in phase C by exactly one lane (the first dW2 / dW3
+  // tile of each workgroup, wave 7 / 6, with the tile's bias column; db1 by wave 5 of the ks = 0 workgroups), and that
+  // lane also applies its RMSprop update in phase D with the gradient still in registers (own slots 0..3: the tile
+  // elements, 4: the bias element; -1: none), so no gradient crosses a workgroup. Tiles past a workgroup's first
+  // (grids of fewer than 64 workgroups) go through the GW exchange instead.
+  // own_index(oi): this lane's owned elements (called where needed, so nothing stays live across the phases)
+  auto own_index = [&](int (&oi)[5], int w, int g, int c, int lane) {
+#pragma unroll
+    for (int s = 0; s < 5; ++s) oi[s] = -1;
+    const int nat = A16 / 16;
+    if (w == 7 && wg < 64) {
+      const int qu = wg >> 3, qj = wg & 7;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) oi[e] = (int)a.o_w2 + (16 * qu + 4 * g + e) * CH + 16 * qj + c;
+      if (qj == 0 && lane < 16) oi[4] = (int)a.o_b2 + 16 * qu + lane;
+    } else if (w == 6 && wg < 8 * nat) {
+      const int qa = wg >> 3, qj = wg & 7;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int arow = 16 * qa + 4 * g + e;
+        if (arow < A) oi[e] = (int)a.o_w3 + arow * CH + 16 * qj + c;
+      }
+      if (qj == 0 && lane < 16 && 16 * qa + c < A) oi[4] = (int)a.o_b3 + 16 * qa + c;
+    } else if (w == 5 && ks == 0 && lane < 16) {
+      oi[4] = (int)a.o_b1 + u0 + lane;
+    }
+  };
   __syncthreads();
 
   // X_t of the next live step, prefetched into registers (plain loads: X is written before the launch)
@@ -248,6 +274,19 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
       }
     }
   };
+  // X_t of the coming step from the prefetch registers into Xs (LDS). Called where Xs is free (after phase C's dW1
+  // reads, before phase D) and the prefetch is known complete (behind phase C's drain), so no wait here and no
+  // phase-D store ever sits in front of it in the wave's memory counter.
+  auto stage_x = [&](int tidv) {
+#pragma unroll
+    for (int q = 0; q < CC_XPT; ++q) {
+      const int e = tidv + CC_THREADS * q, rr = e / CC_XV, k = 4 * (e - rr * CC_XV);
+      if (rr < R) {
+        float* d = &Xs[rr * CC_KP + k];
+        d[0] = xv[q][0]; d[1] = xv[q][1]; d[2] = xv[q][2]; d[3] = xv[q][3];
+      }
+    }
+  };
   // the first live step below `t0` (-1 if none): 64 mask sums per round trip, the highest live one wins
   auto next_live = [&](int t0) {
     for (int base = t0 - 1; base >= 0; base -= 64) {
@@ -257,17 +296,33 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
     }
     return -1;
   };
-  load_x(next_live(T), tid);
+  // the loop walks the live steps only: the next one (and its mask sum) is found during phase B, so no load opens a
+  // step (a load there would wait behind the previous step's phase-D stores: one vmcnt for loads and stores)
+  int t = next_live(T);
+  float mt = t >= 0 ? a.msum[t] : 0.0f;
+  load_x(t, tid);
+  stage_x(tid);
+  for (int e = R * CC_KP + tid; e < CC_MAXR * CC_KP; e += CC_THREADS) Xs[e] = 0.0f;   // rows R ..: zero for good
   int live = 0, last_t = -1;
-  int td_at = 0;
-  float td_m = 0.0f, td_y = 0.0f;
+  // misc: [0, 16) dQ of the head's rows, [16, 32) their actions (as float), [32, 40) phase C's per-wave partials,
+  // [48, 51) phase D's scalars, [63] the poll result, [64, 80) / [80, 96) the rows' masks / TD targets, [96, 176) the
+  // rows' five loss terms
+  float* dqs = misc;
+  float* acts = misc + 16;
   auto stamp = [&](int k) {
     if (a.trace && wg == 0 && tid == 0 && live < 16) a.trace[live * 8 + k] = __builtin_amdgcn_s_memrealtime();
   };
+  // a diagnostic build (-DMQ_COMA_BTRACE, scripts/gpu_ab_coma.sh btrace) moves stamps 3 .. 7 into phase B: H1 (the
+  // fan-in) | H2 | Q + TD | dH2 | dH1, printed under the labels B | bar2 | C | bar3 | D; "next" is then the rest
+#ifdef MQ_COMA_BTRACE
+  auto stamp_b = [&](int k) { stamp(k); };
+  auto stamp_n = [&](int) {};
+#else
+  auto stamp_b = [&](int) {};
+  auto stamp_n = [&](int k) { stamp(k); };
+#endif
   bool ok = true;
-  for (int t = T - 1; t >= 0 && ok; --t) {
-    const float mt = a.msum[t];
-    if (!(mt > 0.0f)) continue;   // uniform: every workgroup skips the same steps
+  while (t >= 0 && ok) {   // uniform: every workgroup walks the same live steps
     stamp(0);
     // per-thread indices recomputed every step: the laundered copy keeps the compiler from hoisting every address
     // derived from them out of the loop (that hoisting spilled ~350 B per thread)
@@ -276,27 +331,22 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
     const int tid = tid_l, w = __builtin_amdgcn_readfirstlane(tid_l >> 6), lane = tid_l & 63, g = lane >> 4,
               c = lane & 15;
     // ================================================================ A: H1 partial pre-activations
-    {
-#pragma unroll
-      for (int q = 0; q < CC_XPT; ++q) {   // X_t[:, slice], loaded into xv while the previous step ran
-        const int e = tid + CC_THREADS * q, rr = e / CC_XV, k = 4 * (e - rr * CC_XV);
-        if (rr < R) {
-          float* d = &Xs[rr * CC_KP + k];
-          d[0] = xv[q][0]; d[1] = xv[q][1]; d[2] = xv[q][2]; d[3] = xv[q][3];
-        }
-      }
+    {   // X_t is in Xs already (staged before the previous step's phase D, or in the prologue)
       if (head && tid < 16) {   // the TD inputs of the head's rows, loaded now so phase B does not wait on them
         const int i = tid, rr = r0 + i;
-        td_at = 0; td_m = 0.0f; td_y = 0.0f;
+        int at = 0;
+        float m = 0.0f, y = 0.0f;
         if (i < nr) {
           const int b = (int)fdiv((uint32_t)rr, a.d.dN), ag = rr - b * n;
           const int64_t slot = a.rp.ep(b) * a.d.t_stride + t;
-          td_at = (int)a.rp.actions[slot * n + ag];
-          td_m = coma_mask(a.rp, slot, t);
-          td_y = a.tgt[(int64_t)t * R + rr];
+          at = (int)a.rp.actions[slot * n + ag];
+          m = coma_mask(a.rp, slot, t);
+          y = a.tgt[(int64_t)t * R + rr];
         }
+        acts[i] = (float)at;
+        misc[64 + i] = m;
+        misc[80 + i] = y;
       }
-      for (int e = R * CC_KP + tid; e < ((R + 15) / 16 * 16) * CC_KP; e += CC_THREADS) Xs[e] = 0.0f;
       __syncthreads();
       const int nrt = (R + 15) / 16;
       if (w < nrt) {   // wave w: rows 16 w .. +15, the whole K slice
@@ -319,7 +369,9 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
     if (!(wg == a.fault_wg && live == 1)) cc_post(a.flagA + wg, (unsigned)(live + 1));
     if (head && !(ok = cc_wait(a, a.flagA, a.NG, (unsigned)(live + 1), misc))) break;
     stamp(2);
-    load_x(next_live(t), tid);   // lands while the heads run phase B
+    const int t_next = next_live(t);
+    const float mt_next = t_next >= 0 ? a.msum[t_next] : 0.0f;
+    load_x(t_next, tid);   // lands while the heads run phase B
     // ================================================================ B: the head of rows r0 .. r0 + 15
     if (head) {
       {   // H1 = relu(sum of the NK slice partials in slice order + b1). Thread = one row x 4 columns (16 x 128 =
@@ -381,12 +433,20 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
         d[0] = h[0]; d[1] = h[1]; d[2] = h[2]; d[3] = h[3];
       }
       __syncthreads();
+      stamp_b(3);
+      // The head's three products take K in lane-group blocks: MFMA step m of lane group g contracts k = 32 g + m
+      // (H2, dH1) or kq kw + (kw / 4) g + m (Q), so each lane reads its A / B operands as 16-B runs of a row.
       if (w < 8) {   // H2 = relu(H1 W2^T + b2): wave w owns unit tile w
         f32x4 acc = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};   // two interleaved chains (even / odd k-steps)
-#pragma unroll 4
-        for (int k = 0; k < CH; k += 8) {
-          acc = mfma_f32_16x4(H1s[c * CC_CP + k + g], W2s[(16 * w + c) * CC_CP + k + g], acc);
-          acc1 = mfma_f32_16x4(H1s[c * CC_CP + k + 4 + g], W2s[(16 * w + c) * CC_CP + k + 4 + g], acc1);
+        const float* ar = H1s + c * CC_CP + 32 * g;
+        const float* br = W2s + (16 * w + c) * CC_CP + 32 * g;
+#pragma unroll
+        for (int mm = 0; mm < 8; ++mm) {
+          const f32x4 av = *(const f32x4*)&ar[4 * mm], bv = *(const f32x4*)&br[4 * mm];
+          acc = mfma_f32_16x4(av[0], bv[0], acc);
+          acc1 = mfma_f32_16x4(av[1], bv[1], acc1);
+          acc = mfma_f32_16x4(av[2], bv[2], acc);
+          acc1 = mfma_f32_16x4(av[3], bv[3], acc1);
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -397,63 +457,56 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
         }
       }
       __syncthreads();
+      stamp_b(4);
       {   // Q = H2 W3^T + b3 on all 8 waves: (action tile qn, K part kq); the K parts' partials meet in dH2s (free
           // until dH2 below) and are summed in kq order
         const int nat = A16 / 16, ksp = 8 / nat, kw = CH / ksp;   // nat in {1, 2}: 8 or 4 K parts of 16 or 32
         const int qn = w % nat, kq = w / nat;
         f32x4 acc = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
-        for (int k = kq * kw; k < (kq + 1) * kw; k += 8) {
-          acc = mfma_f32_16x4(H2s[c * CC_CP + k + g], W3s[(16 * qn + c) * CC_CP + k + g], acc);
-          acc1 = mfma_f32_16x4(H2s[c * CC_CP + k + 4 + g], W3s[(16 * qn + c) * CC_CP + k + 4 + g], acc1);
+        const int kg = kw / 4;   // 4 or 8 k per lane group
+        const float* ar = H2s + c * CC_CP + kq * kw + kg * g;
+        const float* br = W3s + (16 * qn + c) * CC_CP + kq * kw + kg * g;
+        for (int mm = 0; mm < kg; mm += 4) {
+          const f32x4 av = *(const f32x4*)&ar[mm], bv = *(const f32x4*)&br[mm];
+          acc = mfma_f32_16x4(av[0], bv[0], acc);
+          acc1 = mfma_f32_16x4(av[1], bv[1], acc1);
+          acc = mfma_f32_16x4(av[2], bv[2], acc);
+          acc1 = mfma_f32_16x4(av[3], bv[3], acc1);
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) dH2s[(kq * 16 + 4 * g + e) * A16 + 16 * qn + c] = acc[e] + acc1[e];
         __syncthreads();
+        // thread (row i, action j) sums Q[i][j] in kq order; it stores the Q value the actor's baseline uses
+        // (coma_learner.py:126), and the thread of the taken action computes the TD error, dQ and the row's loss
+        // terms (coma_learner.py:124-131)
         if (tid < 16 * A16) {
-          const int i = tid / A16, j = tid - i * A16;
+          const int i = tid / A16, j = tid - i * A16, rr = r0 + i;
           float q = 0.0f;
           for (int p = 0; p < ksp; ++p) q += dH2s[(p * 16 + i) * A16 + j];
-          Qs[i * (A16 + 1) + j] = q + b3s[j];
+          q = q + b3s[j];
+          if (i < nr && j < A) a.qvals[((int64_t)t * R + rr) * A + j] = q;
+          const int at = (int)acts[i];
+          if (j == at) {
+            const float m = misc[64 + i], y = misc[80 + i];
+            float qa = 0.0f, dq = 0.0f, mtd = 0.0f;
+            if (i < nr) {
+              qa = q;
+              mtd = (q - y) * m;
+              dq = (2.0f * mtd) * m;
+              st_wt(&a.dqx[rr], dq);
+              st_wt_i(&a.actx[rr], at);
+            }
+            dqs[i] = dq;
+            misc[96 + i] = mtd * mtd;
+            misc[112 + i] = m;
+            misc[128 + i] = fabsf(mtd);
+            misc[144 + i] = qa * m;
+            misc[160 + i] = y * m;
+          }
         }
       }
       __syncthreads();
-      float* dqs = misc;              // [16]
-      float* acts = misc + 16;        // [16] (action as float)
-      if (tid < 16) {   // TD error, loss sums, dQ at the taken action (coma_learner.py:124-131)
-        const int i = tid, rr = r0 + i;
-        float q = 0.0f, dq = 0.0f, mtd = 0.0f;
-        const int at = td_at;
-        const float m = td_m, y = td_y;
-        if (i < nr) {
-          q = Qs[i * (A16 + 1) + at];
-          mtd = (q - y) * m;
-          dq = (2.0f * mtd) * m;
-          st_wt(&a.dqx[rr], dq);
-          st_wt_i(&a.actx[rr], at);
-        }
-        dqs[i] = dq;
-        acts[i] = (float)at;
-        // the five loss sums over the tile's rows, in row order (the three-launch head's order), staged through
-        // dH2s (written only below): one wave, so its LDS accesses stay in program order
-        const float vals[5] = {mtd * mtd, m, fabsf(mtd), q * m, y * m};
-#pragma unroll
-        for (int kk = 0; kk < 5; ++kk) dH2s[kk * 16 + i] = vals[kk];
-        asm volatile("" ::: "memory");
-        if (i < 5) {
-          float rv[16];
-#pragma unroll
-          for (int j = 0; j < 16; ++j) rv[j] = dH2s[i * 16 + j];
-          float sum = 0.0f;
-#pragma unroll
-          for (int j = 0; j < 16; ++j) sum += rv[j];
-          st_wt(&a.part[wg * 8 + i], sum);
-        }
-      }
-      for (int e = tid; e < 16 * A; e += CC_THREADS) {   // the Q values the actor's baseline uses (coma_learner.py:126)
-        const int i = e / A, aa = e - i * A;
-        if (i < nr) a.qvals[((int64_t)t * R + r0 + i) * A + aa] = Qs[i * (A16 + 1) + aa];
-      }
-      __syncthreads();
+      stamp_b(5);
       for (int e = tid; e < 16 * CH; e += CC_THREADS) {   // dH2 = dQ W3[a] o [H2 > 0]
         const int i = e >> 7, u = e & 127;
         const float h2 = H2s[i * CC_CP + u];
@@ -462,12 +515,18 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
         if (i < nr) st_wt(&a.dH2x[(int64_t)(r0 + i) * CH + u], v);
       }
       __syncthreads();
+      stamp_b(6);
       if (w < 8) {   // dH1 = dH2 W2 o [H1 > 0]: B[kk][j] = W2[kk][j]
         f32x4 acc = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
-#pragma unroll 4
-        for (int k = 0; k < CH; k += 8) {
-          acc = mfma_f32_16x4(dH2s[c * CC_CP + k + g], W2s[(k + g) * CC_CP + 16 * w + c], acc);
-          acc1 = mfma_f32_16x4(dH2s[c * CC_CP + k + 4 + g], W2s[(k + 4 + g) * CC_CP + 16 * w + c], acc1);
+        const float* ar = dH2s + c * CC_CP + 32 * g;
+        const float* br = W2s + (32 * g) * CC_CP + 16 * w + c;
+#pragma unroll
+        for (int mm = 0; mm < 8; ++mm) {
+          const f32x4 av = *(const f32x4*)&ar[4 * mm];
+          acc = mfma_f32_16x4(av[0], br[(4 * mm) * CC_CP], acc);
+          acc1 = mfma_f32_16x4(av[1], br[(4 * mm + 1) * CC_CP], acc1);
+          acc = mfma_f32_16x4(av[2], br[(4 * mm + 2) * CC_CP], acc);
+          acc1 = mfma_f32_16x4(av[3], br[(4 * mm + 3) * CC_CP], acc1);
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -475,17 +534,31 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
           if (i < nr) st_wt(&a.dH1x[(int64_t)(r0 + i) * CH + j], H1s[i * CC_CP + j] > 0.0f ? acc[e] + acc1[e] : 0.0f);
         }
       }
+      if (w == 0 && lane < 5) {   // the five loss sums over the tile's rows, in row order (the three-launch head's)
+        float rv[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) rv[j] = misc[96 + 16 * lane + j];
+        float sum = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sum += rv[j];
+        st_wt(&a.part[wg * 8 + lane], sum);
+      }
+#ifdef MQ_COMA_BTRACE
+      __syncthreads();
+#endif
+      stamp_b(7);
     }
-    stamp(3);
+    stamp_n(3);
     // B -> C: the heads flag H1 / H2 / dH2 / dH1 / dQ / actions / loss partials; every workgroup waits for them
     if (head) cc_post(a.flagB + wg, (unsigned)(live + 1));
     if (!(ok = cc_wait(a, a.flagB, a.NHEAD, (unsigned)(live + 1), misc))) break;
-    stamp(4);
+    stamp_n(4);
     // ================================================================ C: gradients, per-workgroup sum of squares
     float sq = 0.0f;
+    float og[5] = {0, 0, 0, 0, 0};   // the owned elements' raw gradients (own_index order)
     {
-      // operands of the dW2 (wave 7) and dW3 (wave 6) tiles: all CC_MAXR / 4 k-steps of one tile per round trip; the
-      // first tile's loads are issued before the dH1 loads below, so the two round trips overlap
+      // operands of the dW2 (wave 7) and dW3 (wave 6) tiles: all CC_MAXR / 4 k-steps of one tile per round trip, in
+      // flight while the other waves load dH1 and run the dW1 tile
       const int nat = A16 / 16;
       float pA[CC_MAXR / 4], pB[CC_MAXR / 4];
       int pI[CC_MAXR / 4];
@@ -519,7 +592,9 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
         const int rr = tid >> 2, u = 4 * (tid & 3);
         f32x4 dv = {0, 0, 0, 0};
         if (rr < R) dv = ld_wt4(a.dH1x + (int64_t)rr * CH + u0 + u);
-        cc_vm_wait();
+        // only the waves holding rows (16 w < R) wait: the dW2 / dW3 waves (6, 7; rows >= 96) reach the barrier
+        // at once, and their own operand loads are waited for where their MFMAs use them
+        if (16 * w < R) cc_vm_wait();
         cc_ready(dv);
         if (rr < CC_MAXR) {
           float* d = &Du[rr * 17 + u];
@@ -532,9 +607,9 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
         f32x4 acc = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};   // two interleaved k-chains (even / odd 4-row steps)
 #pragma unroll
         for (int q = 0; q < CC_MAXR / 4; ++q) {
-          const int row = 4 * q + g;
-          const float av = row < R ? Du[row * 17 + c] : 0.0f;
-          const float bv = row < R ? Xs[row * CC_KP + 16 * w + c] : 0.0f;
+          const int row = 4 * q + g;   // rows R .. CC_MAXR are zero in both operands
+          const float av = Du[row * 17 + c];
+          const float bv = Xs[row * CC_KP + 16 * w + c];
           if (q & 1) acc1 = mfma_f32_16x4(av, bv, acc1);
           else acc = mfma_f32_16x4(av, bv, acc);
         }
@@ -546,16 +621,24 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
         }
       }
       if (w == 5 && ks == 0) {   // db1 of the owned units: column sums of dH1, in row order
-        if (lane < 16) {
+        if (lane < 16) {   // all CC_MAXR rows (rows R .. are zero), read 16 at a time ahead of the serial sum
           float s = 0.0f;
-          for (int rr = 0; rr < R; ++rr) s += Du[rr * 17 + lane];
-          st_wt(&a.GW[a.o_b1 + u0 + lane], s);
+#pragma unroll
+          for (int r16 = 0; r16 < CC_MAXR; r16 += 16) {
+            float v[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[j] = Du[(r16 + j) * 17 + lane];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) s += v[j];
+          }
+          og[4] = s;
           sq = fmaf(s, s, sq);
         }
       } else if (w == 7) {   // dW2 tiles (16 units x 16 columns, K = rows), round-robin over the workgroups
         for (int qt = wg; qt < 64; qt += a.NG) {
           const int qu = qt >> 3, qj = qt & 7;
-          if (qt != wg) load_w2(qt);
+          const bool first = qt == wg;
+          if (!first) load_w2(qt);
           f32x4 acc = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
           float bs = 0.0f;
 #pragma unroll
@@ -567,14 +650,16 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float gv = acc[e] + acc1[e];
-            st_wt(&a.GW[a.o_w2 + (int64_t)(16 * qu + 4 * g + e) * CH + 16 * qj + c], gv);
+            if (first) og[e] = gv;
+            else st_wt(&a.GW[a.o_w2 + (int64_t)(16 * qu + 4 * g + e) * CH + 16 * qj + c], gv);
             sq = fmaf(gv, gv, sq);
           }
           if (qj == 0) {   // db2 of the tile's units: lane groups g hold rows g, g + 4, ..: combine the four
             bs += __shfl_xor(bs, 16, 64);
             bs += __shfl_xor(bs, 32, 64);
             if (lane < 16) {
-              st_wt(&a.GW[a.o_b2 + 16 * qu + lane], bs);
+              if (first) og[4] = bs;
+              else st_wt(&a.GW[a.o_b2 + 16 * qu + lane], bs);
               sq = fmaf(bs, bs, sq);
             }
           }
@@ -584,7 +669,8 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
         for (int qt = wg; qt < 8 * nat; qt += a.NG) {
           const int qa = qt >> 3, qj = qt & 7;
           const int aa = 16 * qa + c;
-          if (qt != wg) load_w3(qt);
+          const bool first = qt == wg;
+          if (!first) load_w3(qt);
           f32x4 acc = {0, 0, 0, 0};
           float bs = 0.0f;
           f32x4 acc1 = {0, 0, 0, 0};
@@ -600,7 +686,8 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
             const int arow = 16 * qa + 4 * g + e;
             if (arow < A) {
               const float gv = acc[e] + acc1[e];
-              st_wt(&a.GW[a.o_w3 + (int64_t)arow * CH + 16 * qj + c], gv);
+              if (first) og[e] = gv;
+              else st_wt(&a.GW[a.o_w3 + (int64_t)arow * CH + 16 * qj + c], gv);
               sq = fmaf(gv, gv, sq);
             }
           }
@@ -608,7 +695,8 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
             bs += __shfl_xor(bs, 16, 64);
             bs += __shfl_xor(bs, 32, 64);
             if (lane < 16 && aa < A) {
-              st_wt(&a.GW[a.o_b3 + aa], bs);
+              if (first) og[4] = bs;
+              else st_wt(&a.GW[a.o_b3 + aa], bs);
               sq = fmaf(bs, bs, sq);
             }
           }
@@ -617,6 +705,8 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
       sq = wave_sum(sq);
       if (lane == 0) misc[32 + w] = sq;   // misc[32 .. 39]: per-wave partials
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's write-through stores of C drained ...
+#pragma unroll
+      for (int q = 0; q < CC_XPT; ++q) cc_ready(xv[q]);   // (the next step's X prefetch landed with them)
       __syncthreads();
       if (tid == 0) {   // ... before this workgroup's {sum of squares, step tag} granule: its flag for phase D
         float s = 0.0f;
@@ -624,11 +714,27 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
         const unsigned long long gv = ((unsigned long long)(unsigned)(live + 1) << 32) | __float_as_uint(s);
         __hip_atomic_store((cc_gu64*)(a.normg + wg), gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      stage_x(tid);   // Xs is free (the dW1 reads are behind the barrier); phase A reads it after its own barrier
     }
-    stamp(5);
+    // the owned elements' parameter and square_avg (written by this lane only), loaded while wave 0 polls the
+    // granules. Branch-free: buffer accesses whose offset kDrop (no owned element) lies past the range, so every slot
+    // is one instruction on every path and the compiler's wait counts stay exact (with the slots under branches it
+    // waited for each slot's write-through stores before the next slot's math)
+    int oi[5];
+    own_index(oi, w, g, c, lane);
+    const auto prs = buf_rsrc(a.P), srs = buf_rsrc(a.SQ), grs = buf_rsrc(a.G);
+    uint32_t ooff[5];
+    float op[5], os[5];
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+      ooff[s] = oi[s] >= 0 ? (uint32_t)oi[s] * 4u : kDrop;
+      op[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(prs, ooff[s], 0, kCpolSc1));
+      os[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ooff[s], 0, kCpolSc1));
+    }
+    stamp_n(5);
     // no counter barrier here: wave 0 polls the G granules (one 8-B write-through store each, MI355X_MICROARCH.md
     // Valid forms: R2 granules / row 1 flags), and the other waves join behind the workgroup barrier below
-    stamp(6);
+    stamp_n(6);
     // ================================================================ D: clip + RMSprop (coma_learner.py:132-134)
     if (w == 0) {   // the squared norm: each lane sums its partials (lane, lane + 64, ..), then a fixed butterfly
       float pv[4];
@@ -693,19 +799,42 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
         }
       }
     }
-    for (int e = h_beg + tid; e < h_end; e += CC_THREADS) {   // the owned slice of fc1.bias .. fc3.bias
-      const int64_t i = a.o_b1 + e;
-      const float gg = (ld_wt(&a.GW[i]) * inv) * coef;
-      const float v = a.SQ[i] * alpha + (1.0f - alpha) * (gg * gg);
-      st_wt(&a.P[i], ld_wt(&a.P[i]) + (-lr) * (gg / (sqrtf(v) + eps)));   // the heads reload it in phase B
-      a.SQ[i] = v;
-      a.G[i] = gg;   // the last live step's clipped gradient stays
+    // the owned elements of fc1.bias .. fc3.bias, from registers; P write-through (the heads reload it in phase B),
+    // G the last live step's clipped gradient
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+      const float gg = (og[s] * inv) * coef;
+      const float v = os[s] * alpha + (1.0f - alpha) * (gg * gg);
+      const float pn = op[s] + (-lr) * (gg / (sqrtf(v) + eps));
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, pn), prs, ooff[s], 0, kCpolSc1);
+      buf_st(srs, ooff[s], v);
+      buf_st(grs, ooff[s], gg);
+    }
+    if (w >= 6 && wg + a.NG < 64) {   // tiles past the first (grids of fewer than 64 workgroups): via GW
+      auto upd = [&](int64_t i) {
+        const float gg = (ld_wt(&a.GW[i]) * inv) * coef;
+        const float v = a.SQ[i] * alpha + (1.0f - alpha) * (gg * gg);
+        st_wt(&a.P[i], ld_wt(&a.P[i]) + (-lr) * (gg / (sqrtf(v) + eps)));
+        a.SQ[i] = v;
+        a.G[i] = gg;
+      };
+      const int nat = A16 / 16;
+      for (int qt = wg + a.NG; qt < (w == 7 ? 64 : 8 * nat); qt += a.NG) {
+        const int qr = qt >> 3, qj = qt & 7;
+        const int64_t ow = w == 7 ? a.o_w2 : a.o_w3, ob = w == 7 ? a.o_b2 : a.o_b3;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (w == 7 || 16 * qr + 4 * g + e < A) upd(ow + (int64_t)(16 * qr + 4 * g + e) * CH + 16 * qj + c);
+        if (qj == 0 && lane < 16 && (w == 7 || 16 * qr + c < A)) upd(ob + 16 * qr + lane);
+      }
     }
     if (wg == a.NG - 1 && tid == 0) a.crec[t * 8 + 5] = misc[50];   // the step's gradient norm
-    stamp(7);
+    stamp_n(7);
     ++live;
     last_t = t;
-    __syncthreads();
+    t = t_next;
+    mt = mt_next;
+    lds_barrier();   // W1t / misc reuse; the phase-D stores drain behind the next step's work (cc_post waits for them)
   }
   if (!ok || live == 0) {
     if (wg == 0 && tid == 0) { a.cstate[0] = ok ? 0 : -1; a.cstate[1] = 0; }
@@ -724,6 +853,7 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
       }
     }
   }
+
   if (wg == 0 && tid == 0) {   // fc1.bias .. fc3.bias are final in P / SQ / G already
     a.G[a.Pc] = a.msum[last_t];
     a.cstate[0] = live;

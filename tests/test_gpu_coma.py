@@ -174,13 +174,21 @@ def test_coma_chain_matches_three_launch(coma_cases, name, monkeypatch):
     long_chain = c.T > 50
     for k in range(2):
         (sa, ca, qa, va, aa), (sb, cb, qb, vb, ab) = runs["chain"][k], runs["three_launch"][k]
-        assert np.abs(ca - cb).max() <= (1e-3 if long_chain else 1e-5), (name, k)
+        # T = 180 at cfg5: RMSprop's 1 / (sqrt(v) + eps) turns last-bit differences in near-zero gradients into
+        # lr-sized steps, so two summation orders drift apart like either does from the oracle. Measured over one
+        # coma_cfg5 train() (scripts/coma_diff.py, round 6): chain vs oracle 1.9e-3, three-launch vs oracle 3.5e-3,
+        # chain vs three-launch 3.1e-3 (the oracle band of test_coma_teacher_forced is 5e-4 T = 0.09)
+        assert np.abs(ca - cb).max() <= (5e-3 if long_chain else 1e-5), (name, k)
         assert rel(va, vb) < (1e-3 if long_chain else 1e-5), (name, k)
         assert rel(qa, qb) < (1e-2 if long_chain else 1e-4), (name, k)
         assert sa["critic_steps"] == sb["critic_steps"]
         for s in COMA_STATS:
             assert np.isfinite(sa[s]), (name, k, s)
-            assert abs(sa[s] - sb[s]) <= (2e-3 if long_chain else 1e-4) * abs(sb[s]) + 1e-5, (name, k, s, sa[s], sb[s])
+            # the oracle test's bands: the actor-side means of small Q differences get an absolute one
+            tol = (2e-3 if long_chain else 1e-4) * abs(sb[s]) + 1e-5
+            if long_chain and s in ("advantage_mean", "coma_loss"):
+                tol = max(tol, 2e-5)
+            assert abs(sa[s] - sb[s]) <= tol, (name, k, s, sa[s], sb[s])
 
 
 @pytest.mark.parametrize("path,env", [("chain", None), ("three_launch", "0")])
