@@ -4,7 +4,7 @@
 // G = 8 * NK workgroups of 512 threads, all resident (G <= the CU count, one per CU). Workgroup (ut, ks) owns the W1
 // tile [16 units ut][CC_KW columns ks] for the whole train: the tile stays in LDS and its RMSprop square_avg and
 // gradient in registers, so W1 (the critic's 111k-element bulk at MMM2) never leaves the CU between steps. The first
-// NHEAD = ceil(R / 16) workgroups also run the head of one 16-row tile. fc1.bias / fc2 / fc3 live in P (the caller's
+// NHEAD = ceil(R / 16) workgroups (grouped on as few XCDs as possible) also run the head of one 16-row tile. fc1.bias / fc2 / fc3 live in P (the caller's
 // buffer): the lane that computes an element's gradient in phase C applies its update in place in phase D, and the
 // heads reload the new version into LDS at the start of the next step. One live step t is four phases:
 //   A  (all)   H1p[ks][r][16 ut ..] = X_t[r][K slice] W1_tile^T                         (MFMA; X_t prefetched)
@@ -204,8 +204,13 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
   const int wg = blockIdx.x, ut = wg & 7, ks = wg >> 3;
   const int u0 = 16 * ut, k0 = ks * CC_KW;
   const int kwc = max(0, min(CC_KW, Kc - k0));       // real W1 columns of this tile
-  const bool head = wg < a.NHEAD;
-  const int r0 = 16 * wg, nr = head ? min(16, R - r0) : 0;
+  // head slot hs of this workgroup: slot-major within an XCD (blocks b and b + 8 share one, MI355X_MICROARCH.md
+  // § dispatch), so the heads (hs < NHEAD) sit on as few XCDs as the grid allows and their per-step reload of
+  // fc1.bias .. fc3.bias, 76 KB each, is served by one L2 after the first miss (placement only: correctness does
+  // not depend on it)
+  const int hs = (wg & 7) * a.NK + (wg >> 3);
+  const bool head = hs < a.NHEAD;
+  const int r0 = 16 * hs, nr = head ? min(16, R - r0) : 0;
   const int npart = (int)(a.Pc - a.o_b1);            // b1 .. b3, contiguous
   const float alpha = a.hp.alpha, lr = a.hp.lr, eps = a.hp.eps;
 
@@ -541,7 +546,7 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
         float sum = 0.0f;
 #pragma unroll
         for (int j = 0; j < 16; ++j) sum += rv[j];
-        st_wt(&a.part[wg * 8 + lane], sum);
+        st_wt(&a.part[hs * 8 + lane], sum);
       }
 #ifdef MQ_COMA_BTRACE
       __syncthreads();
@@ -550,7 +555,7 @@ __global__ __launch_bounds__(CC_THREADS) void coma_chain_kernel(CChain a) {
     }
     stamp_n(3);
     // B -> C: the heads flag H1 / H2 / dH2 / dH1 / dQ / actions / loss partials; every workgroup waits for them
-    if (head) cc_post(a.flagB + wg, (unsigned)(live + 1));
+    if (head) cc_post(a.flagB + hs, (unsigned)(live + 1));
     if (!(ok = cc_wait(a, a.flagB, a.NHEAD, (unsigned)(live + 1), misc))) break;
     stamp_n(4);
     // ================================================================ C: gradients, per-workgroup sum of squares
